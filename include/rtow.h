@@ -1,0 +1,288 @@
+/*
+ * rtow.h — C-ABI of the MI355X path tracer (librtow_hip.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel render loop,
+ * raytraceWorkerProcedure main.cpp:932-996.  The reference has
+ * no FFI; the seam is that loop body, whose inputs are RenderProperties
+ * (common.h:10-15), a Camera* (camera.h:10), a Hitable* world and a
+ * WorkerImageBuffer (common.h:17-21) it writes in place.  Here:
+ *
+ *   Hitable* world         -> rtow_scene   (the object graph, flattened 1:1)
+ *   Camera*                -> rtow_camera  (the basis camera.h:315-342 builds)
+ *   RenderProperties       -> rtow_params
+ *   WorkerImageBuffer      -> bgra_out     (W*H*4 bytes, layout main.cpp:982-989)
+ *
+ * Plain C types only: pointers, sizes, PODs.  Every function returns 0 on
+ * success or a negative RTOW_E* code (rtow_error_string()); HIP errors are
+ * reported as RTOW_E_HIP and the HIP message is kept for rtow_last_error().
+ *
+ * Scene-graph flattening order (so two producers of the same world produce
+ * byte-identical rtow_scene arrays): depth-first pre-order from the root,
+ * memoised by object identity (a shared object is emitted once and referenced
+ * by index).  A hitable gets its index before its children are visited.
+ * Children order: BvhNode left, right; HitableList items in order (the list's
+ * refs range is reserved before its items are visited); Box -> its 6-side list;
+ * FlipNormals/Translate/RotateY -> child; ConstantMedium -> boundary, then the
+ * phase material.  Materials and textures are numbered at first use, in that
+ * same walk; a CheckerTexture visits odd, then even.  Unused fields are zero.
+ */
+#ifndef RTOW_H
+#define RTOW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTOW_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------- */
+enum {
+    RTOW_OK = 0,
+    RTOW_E_INVALID = -1,      /* bad argument / inconsistent scene */
+    RTOW_E_UNSUPPORTED = -2,  /* scene construct the device path does not handle */
+    RTOW_E_HIP = -3,          /* a HIP runtime call failed */
+    RTOW_E_NO_DEVICE = -4,    /* no GPU visible */
+    RTOW_E_IO = -5,           /* file read/write failed */
+    RTOW_E_NOMEM = -6
+};
+
+/* ---- scene graph ---------------------------------------------------------- */
+
+/* One record per reference Hitable object.  Field use per kind:
+ *   SPHERE         sphere.h:7-18       f[0..2] center, f[3] radius, a material
+ *   MOVING_SPHERE  sphere.h:76-91      f[0..2] center0, f[3..5] center1,
+ *                                      f[6] time0, f[7] time1, f[8] radius, a material
+ *   RECT_XY        xy_rect.h:7-20      f[0] x0 f[1] x1 f[2] y0 f[3] y1 f[4] k, a material
+ *   RECT_XZ        xy_rect.h:42-55     f[0] x0 f[1] x1 f[2] z0 f[3] z1 f[4] k, a material
+ *   RECT_YZ        xy_rect.h:77-90     f[0] y0 f[1] y1 f[2] z0 f[3] z1 f[4] k, a material
+ *   FLIP_NORMALS   hitable.h:25-42     a child
+ *   TRANSLATE      hitable.h:44-51     a child, f[0..2] offset
+ *   ROTATE_Y       hitable.h:74-88     a child, b hasBox, f[0] sinTheta, f[1] cosTheta,
+ *                                      f[2..4] box min, f[5..7] box max
+ *   LIST           hitableList.h:7-18  a first index in refs[], b count
+ *   BOX            box.h:10-23         a its 6-side LIST, f[0..2] pMin, f[3..5] pMax
+ *   BVH_NODE       bvhNode.h:12-23     a left, b right, f[0..2] box min, f[3..5] box max
+ *   CONSTANT_MEDIUM constantMedium.h:10-24  a boundary, b phase material (ISOTROPIC),
+ *                                      f[0] density
+ */
+enum {
+    RTOW_HIT_SPHERE = 1,
+    RTOW_HIT_MOVING_SPHERE = 2,
+    RTOW_HIT_RECT_XY = 3,
+    RTOW_HIT_RECT_XZ = 4,
+    RTOW_HIT_RECT_YZ = 5,
+    RTOW_HIT_FLIP_NORMALS = 6,
+    RTOW_HIT_TRANSLATE = 7,
+    RTOW_HIT_ROTATE_Y = 8,
+    RTOW_HIT_LIST = 9,
+    RTOW_HIT_BOX = 10,
+    RTOW_HIT_BVH_NODE = 11,
+    RTOW_HIT_CONSTANT_MEDIUM = 12
+};
+
+typedef struct rtow_hitable {
+    uint32_t kind, a, b, c;
+    float f[12];
+} rtow_hitable; /* 64 bytes */
+
+/* material.h:43-148.  LAMBERTIAN/DIFFUSE_LIGHT/ISOTROPIC use `texture`;
+ * METAL uses albedo[] and param (= fuzz, already clamped to <= 1 as the
+ * constructor material.h:60 does); DIELECTRIC uses param (= refIndex). */
+enum {
+    RTOW_MAT_LAMBERTIAN = 1,
+    RTOW_MAT_METAL = 2,
+    RTOW_MAT_DIELECTRIC = 3,
+    RTOW_MAT_DIFFUSE_LIGHT = 4,
+    RTOW_MAT_ISOTROPIC = 5
+};
+
+typedef struct rtow_material {
+    uint32_t kind, texture;
+    float param;
+    float albedo[3];
+    uint32_t pad[2];
+} rtow_material; /* 32 bytes */
+
+/* texture.h:11-79.  CONSTANT f[0..2] color; CHECKER a odd, b even;
+ * NOISE f[0] scale, a filter flag; IMAGE a image index. */
+enum {
+    RTOW_TEX_CONSTANT = 1,
+    RTOW_TEX_CHECKER = 2,
+    RTOW_TEX_NOISE = 3,
+    RTOW_TEX_IMAGE = 4
+};
+
+typedef struct rtow_texture {
+    uint32_t kind, a, b, c;
+    float f[4];
+} rtow_texture; /* 32 bytes */
+
+/* An RGB8 image as stbi_load returns it (scenes.h:140): nx*ny*3 bytes, row 0
+ * first, at texels + offset. */
+typedef struct rtow_image {
+    uint32_t nx, ny, channels, pad;
+    uint64_t offset;
+} rtow_image; /* 24 bytes */
+
+/* The static Perlin tables (noise.h:51-55, generated at noise.h:112-116). */
+typedef struct rtow_perlin {
+    float ranfloat[256];
+    float ranvec[256][3];
+    int32_t perm_x[256];
+    int32_t perm_y[256];
+    int32_t perm_z[256];
+} rtow_perlin;
+
+typedef struct rtow_scene {
+    uint32_t root;
+    uint32_t n_hitables;
+    const rtow_hitable* hitables;
+    uint32_t n_refs;
+    const uint32_t* refs;
+    uint32_t n_materials;
+    const rtow_material* materials;
+    uint32_t n_textures;
+    const rtow_texture* textures;
+    const rtow_perlin* perlin;
+    uint32_t n_images;
+    const rtow_image* images;
+    uint64_t n_texel_bytes;
+    const uint8_t* texels;
+} rtow_scene;
+
+/* ---- camera ----------------------------------------------------------------
+ * The state Camera::getRay (camera.h:123-135) reads, as
+ * setCamera_QuaternionMatrix (camera.h:315-342) leaves it. */
+typedef struct rtow_camera {
+    float origin[3];
+    float lower_left_corner[3];
+    float horizontal[3];
+    float vertical[3];
+    float u[3], v[3], w[3];
+    float lens_radius;
+    float time0, time1;
+} rtow_camera;
+
+/* ---- render parameters -----------------------------------------------------
+ * Defaults (rtow_params_default) reproduce defines.h:23-27:
+ * GLOBAL_ILLUM_EN 1, SKY_ILLUM_GAIN 1.0, GLOBAL_ILLUM_GAIN 0.3,
+ * DEPTH_RECURSION 50.  Pixels are grouped in 8x8 tiles (tile t covers
+ * columns 8*(t % tiles_x) .. and rows counted from the TOP of the image);
+ * rank r of `world` renders tiles r, r+world, r+2*world, ... (the reference's
+ * column interleave main.cpp:936, done by tiles). */
+enum {
+    RTOW_FLAG_STATS = 1u << 0 /* count segments (color() calls) on device */
+};
+
+typedef struct rtow_params {
+    uint32_t width, height;
+    uint32_t spp;               /* antiAliasingSamplesPerPixel */
+    uint32_t max_depth;         /* DEPTH_RECURSION */
+    uint32_t gi_enable;         /* GLOBAL_ILLUM_EN */
+    float sky_gain;             /* SKY_ILLUM_GAIN */
+    float gi_gain;              /* GLOBAL_ILLUM_GAIN */
+    uint32_t samples_per_chunk; /* work granularity; 0 = auto (64) */
+    uint64_t seed;              /* render stream seed (rtow_rng.h) */
+    uint32_t rank, world;       /* tile partition; world 0 is treated as 1 */
+    uint32_t flags;
+    uint32_t blocks_per_cu;     /* persistent-grid occupancy; 0 = auto */
+} rtow_params;
+
+typedef struct rtow_stats {
+    uint64_t segments;   /* ray segments traced = reference color() calls */
+    uint64_t samples;    /* paths (pixel samples) traced */
+    uint64_t pixels;     /* pixels this call produced */
+    double kernel_ms;    /* trace kernel, HIP events on the render stream */
+    double resolve_ms;   /* chunk-sum + quantise kernel */
+    double total_ms;     /* whole call, host wall clock */
+} rtow_stats;
+
+/* ---- library ---------------------------------------------------------------- */
+int rtow_abi_version(void);
+const char* rtow_error_string(int code);
+const char* rtow_last_error(void);
+void rtow_params_default(rtow_params* p, uint32_t width, uint32_t height, uint32_t spp);
+
+/* Number of tiles of an image, and how many of them rank r of world renders. */
+uint32_t rtow_tile_count(uint32_t width, uint32_t height);
+uint32_t rtow_rank_tile_count(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
+
+/* ---- host-side scene construction (replaces scenes.h + main.cpp:111-137) --- */
+enum {
+    RTOW_SCENE_THREE_SPHERE = 1,  /* config 1: three Lambertian spheres (composed) */
+    RTOW_SCENE_RANDOM_NED = 2,    /* randomScene_NED scenes.h:122-218, n parameterised */
+    RTOW_SCENE_CORNELL_NED = 3,   /* cornellBox_NED scenes.h:355-483 */
+    RTOW_SCENE_CORNELL_SMOKE = 4  /* cornellBox_NED + smoke box of scenes.h:461-470 */
+};
+
+enum {
+    RTOW_IMAGE_NONE = 0,       /* stbi_load failed: the reference's glass fallback */
+    RTOW_IMAGE_SYNTHETIC = 1,  /* rtow_synthetic_image(2048, 1024) */
+    RTOW_IMAGE_RAW = 2         /* RGB8 raw file image_path, image_nx * image_ny * 3 */
+};
+
+typedef struct rtow_build_opts {
+    uint64_t scene_seed;       /* rtow_scene_key(scene_seed) drives Perlin + scene draws */
+    uint32_t n;                /* randomScene_NED's n (reference: 100) */
+    uint32_t image_mode;
+    const char* image_path;
+    uint32_t image_nx, image_ny;
+    uint32_t wrap_world;       /* 1: add main.cpp's root Translate (main.cpp:132/136) */
+} rtow_build_opts;
+
+typedef struct rtow_scene_buf rtow_scene_buf; /* owns the arrays an rtow_scene views */
+
+void rtow_build_opts_default(rtow_build_opts* o);
+int rtow_build_scene(int scene_id, const rtow_build_opts* opts, rtow_scene_buf** out);
+const rtow_scene* rtow_scene_view(const rtow_scene_buf* buf);
+void rtow_scene_free(rtow_scene_buf* buf);
+int rtow_scene_save(const rtow_scene* scene, const char* path);
+int rtow_scene_load(const char* path, rtow_scene_buf** out);
+/* Number of random-stream draws the last rtow_build_scene consumed (diagnostic). */
+uint32_t rtow_scene_draws(const rtow_scene_buf* buf);
+
+/* The camera main.cpp:111-125 constructs for a width x height frame. */
+int rtow_camera_main(uint32_t width, uint32_t height, rtow_camera* out);
+/* Fill an RGB8 image with the synthetic "earth" stand-in. */
+void rtow_synthetic_image(uint32_t nx, uint32_t ny, uint8_t* rgb);
+
+/* ---- device path ------------------------------------------------------------ */
+typedef struct rtow_context rtow_context;
+
+int rtow_device_count(int* count);
+int rtow_context_create(int device, rtow_context** out);
+int rtow_context_destroy(rtow_context* ctx);
+/* Convert the scene graph to the device layout and copy it to HBM. */
+int rtow_scene_upload(rtow_context* ctx, const rtow_scene* scene);
+
+/* Drop-in for main.cpp:932-996 on one GPU: render every pixel, write the BGRA
+ * frame (host memory, W*H*4, alpha 0) and, if linear_out is not NULL, the
+ * averaged linear RGB before sqrt/quantise (W*H*3 floats, same pixel order).
+ * Synchronous. */
+int rtow_render(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
+                uint8_t* bgra_out, float* linear_out, rtow_stats* stats);
+
+/* Render this rank's tiles (p->rank of p->world) into compact DEVICE slabs:
+ * tile-slot s of the rank holds global tile rank + s*world, 64 pixels row-major
+ * inside the tile; d_bgra_slab gets 4 bytes per pixel, d_linear_slab (may be
+ * NULL) 3 floats.  Enqueued on `stream` (a hipStream_t, NULL = the context's
+ * own); returns after the work completes. */
+int rtow_render_tiles_device(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
+                             void* d_bgra_slab, void* d_linear_slab, void* stream,
+                             rtow_stats* stats);
+
+/* Scatter the gathered slabs of all `world` ranks (rank-major, each
+ * rtow_rank_tile_count(...) * 64 pixels; equal-size padding allowed via
+ * slab_stride_px) into a device BGRA frame. */
+int rtow_assemble_device(rtow_context* ctx, uint32_t width, uint32_t height, uint32_t world,
+                         const void* d_slabs, uint32_t slab_stride_px, void* d_bgra_frame,
+                         void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTOW_H */

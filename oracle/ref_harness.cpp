@@ -1,0 +1,510 @@
+// ref_harness.cpp — TEST INFRASTRUCTURE ONLY (builds into oracle/_ref/, never
+// shipped, never linked into the product).
+//
+// Compiles the reference's own hot-path headers, unmodified, straight from
+// /root/reference/rayTracingOneWeekend (-I on the g++ line, see Makefile) and
+// uses them to produce the golden fixtures in tests/golden/:
+//   * the scene graph the reference builds (scenes.h), flattened to the
+//     rtow_scene layout of include/rtow.h by walking the reference objects;
+//   * the camera basis (camera.h:315-342);
+//   * rendered images: the loop of main.cpp:932-996 re-stated below (main.cpp
+//     itself is Win32-only), calling the reference's Camera::getRay and color().
+//
+// The reference's RNG (rngs.h:9, one global std::mt19937_64 seeded from the
+// clock) is replaced WITHOUT editing any reference file: `mt19937_64` is
+// #defined to an engine that returns rtow_draw24(key, ctr++) << 40 from
+// thread-local (key, ctr), so uniform_real_distribution<double> yields exactly
+// r24 * 2^-24 (include/rtow_rng.h).  The loop sets key = rtow_sample_key(seed,
+// row*W + column, sample), ctr = 0 before each sample's jitter draws.
+//
+// Usage:
+//   ref_harness dump   <scene> <out.scn> [opts]
+//   ref_harness camera <W> <H> <out.cam>
+//   ref_harness render <scene> <W> <H> <spp> <out_prefix> [opts]
+//       writes <out_prefix>.lin (W*H*3 float32, framebuffer order) and
+//       <out_prefix>.bgra (W*H*4 bytes, main.cpp:982-989)
+// scenes: three_sphere | random_ned | cornell | cornell_smoke
+// opts:   --n N  --scene-seed S  --seed S  --threads T  --cwd DIR
+// The scene stream seed is read from RTOW_SCENE_SEED (environment) because the
+// Perlin tables are drawn during static initialisation (noise.h:112-116),
+// before main() runs.
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <limits>
+#include <map>
+#include <memory>
+#include <random>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+#include <unistd.h>
+
+#include "../include/rtow.h"
+#include "../include/rtow_rng.h"
+
+static uint64_t harness_env_scene_key() {
+    const char* s = std::getenv("RTOW_SCENE_SEED");
+    uint64_t seed = s ? std::strtoull(s, nullptr, 0) : 1ull;
+    return rtow_scene_key(seed);
+}
+
+struct CbEngine {
+    using result_type = uint64_t;
+    static constexpr uint64_t min() { return 0; }
+    static constexpr uint64_t max() { return ~0ull; }
+    static thread_local uint64_t key;
+    static thread_local uint32_t ctr;
+    static thread_local uint64_t total;
+    uint64_t operator()() {
+        ++total;
+        return (uint64_t)rtow_draw24(key, ctr++) << 40;
+    }
+    void seed(uint64_t) {}
+    template <class S> void seed(S&) {}
+};
+thread_local uint64_t CbEngine::key = harness_env_scene_key();
+thread_local uint32_t CbEngine::ctr = 0;
+thread_local uint64_t CbEngine::total = 0;
+namespace std { using cbrng_engine = ::CbEngine; }
+#define mt19937_64 cbrng_engine
+
+// The camera basis is private (camera.h:352-379); the harness reads it.
+#define private public
+#define protected public
+#include "defines.h"
+#include "vec3.h"
+#include "scenes.h"
+#undef private
+#undef protected
+
+// ---------------------------------------------------------------------------
+// Scene graph writer: reference objects -> rtow_scene arrays (include/rtow.h
+// documents the canonical order).
+struct GraphWriter {
+    std::vector<rtow_hitable> hit;
+    std::vector<uint32_t> refs;
+    std::vector<rtow_material> mats;
+    std::vector<rtow_texture> texs;
+    std::vector<rtow_image> imgs;
+    std::vector<uint8_t> texels;
+    std::map<const void*, uint32_t> hmap, mmap, tmap, imap;
+
+    static void v3(float* d, const vec3& v) { d[0] = v.x(); d[1] = v.y(); d[2] = v.z(); }
+
+    uint32_t image(const unsigned char* data, int nx, int ny) {
+        auto it = imap.find(data);
+        if (it != imap.end()) return it->second;
+        uint32_t idx = (uint32_t)imgs.size();
+        rtow_image im{};
+        im.nx = (uint32_t)nx; im.ny = (uint32_t)ny; im.channels = 3;
+        im.offset = texels.size();
+        texels.insert(texels.end(), data, data + (size_t)nx * ny * 3);
+        imgs.push_back(im);
+        imap[data] = idx;
+        return idx;
+    }
+
+    uint32_t texture(const Texture* t) {
+        auto it = tmap.find(t);
+        if (it != tmap.end()) return it->second;
+        uint32_t idx = (uint32_t)texs.size();
+        texs.push_back(rtow_texture{});
+        tmap[t] = idx;
+        rtow_texture r{};
+        if (auto c = dynamic_cast<const ConstantTexture*>(t)) {
+            r.kind = RTOW_TEX_CONSTANT; v3(r.f, c->_color);
+        } else if (auto k = dynamic_cast<const CheckerTexture*>(t)) {
+            r.kind = RTOW_TEX_CHECKER;
+            r.a = texture(k->_odd);
+            r.b = texture(k->_even);
+        } else if (auto n = dynamic_cast<const NoiseTexture*>(t)) {
+            r.kind = RTOW_TEX_NOISE; r.f[0] = n->_scaled; r.a = n->_filter ? 1 : 0;
+        } else if (auto im = dynamic_cast<const ImageTexture*>(t)) {
+            r.kind = RTOW_TEX_IMAGE; r.a = image(im->_data, im->_nx, im->_ny);
+        } else {
+            std::fprintf(stderr, "unknown texture\n"); std::exit(3);
+        }
+        texs[idx] = r;
+        return idx;
+    }
+
+    uint32_t material(const Material* m) {
+        auto it = mmap.find(m);
+        if (it != mmap.end()) return it->second;
+        uint32_t idx = (uint32_t)mats.size();
+        mats.push_back(rtow_material{});
+        mmap[m] = idx;
+        rtow_material r{};
+        if (auto l = dynamic_cast<const Lambertian*>(m)) {
+            r.kind = RTOW_MAT_LAMBERTIAN; r.texture = texture(l->_albedo);
+        } else if (auto me = dynamic_cast<const Metal*>(m)) {
+            r.kind = RTOW_MAT_METAL; v3(r.albedo, me->_albedo); r.param = me->_fuzz;
+        } else if (auto d = dynamic_cast<const Dielectric*>(m)) {
+            r.kind = RTOW_MAT_DIELECTRIC; r.param = d->_refIndex;
+        } else if (auto dl = dynamic_cast<const DiffuseLight*>(m)) {
+            r.kind = RTOW_MAT_DIFFUSE_LIGHT; r.texture = texture(dl->_emit);
+        } else if (auto is = dynamic_cast<const Isotropic*>(m)) {
+            r.kind = RTOW_MAT_ISOTROPIC; r.texture = texture(is->_albedo);
+        } else {
+            std::fprintf(stderr, "unknown material\n"); std::exit(3);
+        }
+        mats[idx] = r;
+        return idx;
+    }
+
+    uint32_t hitable(const Hitable* h) {
+        auto it = hmap.find(h);
+        if (it != hmap.end()) return it->second;
+        uint32_t idx = (uint32_t)hit.size();
+        hit.push_back(rtow_hitable{});
+        hmap[h] = idx;
+        rtow_hitable r{};
+        if (auto s = dynamic_cast<const Sphere*>(h)) {
+            r.kind = RTOW_HIT_SPHERE; v3(r.f, s->_center); r.f[3] = s->_radius;
+            r.a = material(s->_materialPointer);
+        } else if (auto s = dynamic_cast<const MovingSphere*>(h)) {
+            r.kind = RTOW_HIT_MOVING_SPHERE; v3(r.f, s->_center0); v3(r.f + 3, s->_center1);
+            r.f[6] = s->_time0; r.f[7] = s->_time1; r.f[8] = s->_radius;
+            r.a = material(s->_materialPointer);
+        } else if (auto q = dynamic_cast<const XYRectangle*>(h)) {
+            r.kind = RTOW_HIT_RECT_XY;
+            r.f[0] = q->_x0; r.f[1] = q->_x1; r.f[2] = q->_y0; r.f[3] = q->_y1; r.f[4] = q->_k;
+            r.a = material(q->_material);
+        } else if (auto q = dynamic_cast<const XZRectangle*>(h)) {
+            r.kind = RTOW_HIT_RECT_XZ;
+            r.f[0] = q->_x0; r.f[1] = q->_x1; r.f[2] = q->_z0; r.f[3] = q->_z1; r.f[4] = q->_k;
+            r.a = material(q->_material);
+        } else if (auto q = dynamic_cast<const YZRectangle*>(h)) {
+            r.kind = RTOW_HIT_RECT_YZ;
+            r.f[0] = q->_y0; r.f[1] = q->_y1; r.f[2] = q->_z0; r.f[3] = q->_z1; r.f[4] = q->_k;
+            r.a = material(q->_material);
+        } else if (auto fl = dynamic_cast<const FlipNormals*>(h)) {
+            r.kind = RTOW_HIT_FLIP_NORMALS; r.a = hitable(fl->_hitable);
+        } else if (auto tr = dynamic_cast<const Translate*>(h)) {
+            r.kind = RTOW_HIT_TRANSLATE; v3(r.f, tr->_offset); r.a = hitable(tr->_hitablePointer);
+        } else if (auto ro = dynamic_cast<const RotateY*>(h)) {
+            r.kind = RTOW_HIT_ROTATE_Y; r.f[0] = ro->_sinTheta; r.f[1] = ro->_cosTheta;
+            r.b = ro->_hasBox ? 1 : 0;
+            v3(r.f + 2, ro->_boundBox.min()); v3(r.f + 5, ro->_boundBox.max());
+            r.a = hitable(ro->_pointer);
+        } else if (auto li = dynamic_cast<const HitableList*>(h)) {
+            r.kind = RTOW_HIT_LIST;
+            r.a = (uint32_t)refs.size(); r.b = li->_listSize;
+            refs.resize(refs.size() + li->_listSize);
+            for (uint32_t i = 0; i < li->_listSize; i++) {
+                uint32_t c = hitable(li->_hitableList[i]);
+                refs[r.a + i] = c;
+            }
+        } else if (auto bx = dynamic_cast<const Box*>(h)) {
+            r.kind = RTOW_HIT_BOX; v3(r.f, bx->_pMin); v3(r.f + 3, bx->_pMax);
+            r.a = hitable(bx->_hitableList);
+        } else if (auto bv = dynamic_cast<const BvhNode*>(h)) {
+            r.kind = RTOW_HIT_BVH_NODE; v3(r.f, bv->_box.min()); v3(r.f + 3, bv->_box.max());
+            r.a = hitable(bv->_left);
+            r.b = hitable(bv->_right);
+        } else if (auto cm = dynamic_cast<const ConstantMedium*>(h)) {
+            r.kind = RTOW_HIT_CONSTANT_MEDIUM; r.f[0] = cm->_density;
+            r.a = hitable(cm->_boundary);
+            r.b = material(cm->_phaseFunction);
+        } else {
+            std::fprintf(stderr, "unknown hitable\n"); std::exit(3);
+        }
+        hit[idx] = r;
+        return idx;
+    }
+
+    void write(const char* path, uint32_t root) {
+        FILE* f = std::fopen(path, "wb");
+        if (!f) { std::perror(path); std::exit(2); }
+        rtow_perlin pt{};
+        for (int i = 0; i < 256; i++) {
+            pt.ranfloat[i] = Perlin::randFloat[i];
+            pt.ranvec[i][0] = Perlin::randVector[i].x();
+            pt.ranvec[i][1] = Perlin::randVector[i].y();
+            pt.ranvec[i][2] = Perlin::randVector[i].z();
+            pt.perm_x[i] = Perlin::permX[i];
+            pt.perm_y[i] = Perlin::permY[i];
+            pt.perm_z[i] = Perlin::permZ[i];
+        }
+        uint32_t hdr[10] = {1u, root, (uint32_t)hit.size(), (uint32_t)refs.size(),
+                            (uint32_t)mats.size(), (uint32_t)texs.size(), (uint32_t)imgs.size(), 1u,
+                            0u, 0u};
+        uint64_t ntex = texels.size();
+        std::fwrite("RTOWSCN1", 1, 8, f);
+        std::fwrite(hdr, 4, 10, f);
+        std::fwrite(&ntex, 8, 1, f);
+        std::fwrite(hit.data(), sizeof(rtow_hitable), hit.size(), f);
+        std::fwrite(refs.data(), 4, refs.size(), f);
+        std::fwrite(mats.data(), sizeof(rtow_material), mats.size(), f);
+        std::fwrite(texs.data(), sizeof(rtow_texture), texs.size(), f);
+        std::fwrite(&pt, sizeof(pt), 1, f);
+        std::fwrite(imgs.data(), sizeof(rtow_image), imgs.size(), f);
+        std::fwrite(texels.data(), 1, texels.size(), f);
+        std::fclose(f);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Scene composition.  Scenes the reference provides are called directly;
+// configurations BASELINE.json names but the reference has no function for are
+// composed from reference classes and documented here.
+
+// randomScene_NED with n other than its hard-coded 100 (scenes.h:124): the same
+// construction, with every random draw sequenced explicitly in the order g++
+// evaluates the reference's expressions (checked: at n = 100 this produces a
+// scene graph byte-identical to the reference's own randomScene_NED()).
+static double U() { return unifRand(randomNumberGenerator); }
+
+static Hitable* randomSceneNedN(int n, bool* usedImage) {
+    Hitable** list = new Hitable*[n + 1];
+    Texture* checker = new CheckerTexture(new ConstantTexture(vec3(0.2, 0.2, 0.8)),
+                                          new ConstantTexture(vec3(0.9, 0.9, 0.9)));
+    Texture* perlin = new NoiseTexture(true, 8.0f);
+    Material* emitterMat = new DiffuseLight(new ConstantTexture(vec3(20, 0, 0)));
+    int nx = 0, ny = 0, nn = 0;
+    unsigned char* texData = stbi_load("./input_images/1_earth_8k.jpg", &nx, &ny, &nn, 0);
+    Material* imageMat = new Lambertian(new ImageTexture(texData, nx, ny));
+    const float R = 1000.0f;
+    const float zOff = -1 * R;
+    list[0] = new Sphere(vec3(0, 0, 0), R, new Lambertian(perlin));
+    int i = 1;
+    const int xMod = 10, yMod = 10;
+    int cx = xMod, cy = yMod;
+    while (i < n - 3) {
+        float choose = (float)U();
+        double uy = U();  // g++ evaluates the vec3 constructor's arguments right to left
+        double ux = U();
+        vec3 center(cx * ux, cy * uy, zOff - 1);
+        if ((center - vec3(4, 0.2, 0)).length() > 0.9) {
+            if (choose < 0.8) {
+                double up = U();
+                list[i++] = new MovingSphere(center, center + vec3(0, 0.5 * up, 0), 0.0, 1.0, 0.2,
+                                             new Lambertian(checker));
+            } else if (choose < 0.95) {
+                double az = U();  // albedo arguments right to left, then the fuzz
+                double ay = U();
+                double ax = U();
+                double fz = U();
+                list[i++] = new Sphere(center, 0.2,
+                                       new Metal(vec3(0.5 * (1 + ax), 0.5 * (1 + ay), 0.5 * (1 + az)),
+                                                 0.5 * (1 + fz)));
+            } else {
+                list[i++] = new Sphere(center, 0.5, new Dielectric(1.5));
+            }
+        }
+        if (cx < xMod) cx++; else { cx = -xMod; cy++; }
+        if (cy > yMod) cy = -yMod;
+    }
+    *usedImage = texData != nullptr;
+    if (texData)
+        list[i++] = new Sphere(vec3(20.0, 0.0, zOff - 25.0), 10.0, imageMat);
+    else
+        list[i++] = new Sphere(vec3(20.0, 0.0, zOff - 25.0), 10.0, new Dielectric(1.5));
+    list[i++] = new Sphere(vec3(100, -70, zOff), 50.0, new Lambertian(perlin));
+    list[i++] = new Sphere(vec3(100, 70, zOff), 50.0, new Metal(vec3(0.7, 0.6, 0.5), 0.0));
+    list[i++] = new Sphere(vec3(0, 0, zOff - 500), 100.0, emitterMat);
+    return new BvhNode(list, i, 0.0, 1.0);
+}
+
+// Config 1: "three-sphere lambertian scene" has no reference function; three
+// Sphere + Lambertian(ConstantTexture) in a HitableList, NED frame, in view of
+// the main.cpp camera (which looks down +x, main.cpp:111-125, camera.h:76-81).
+static Hitable* threeSphereNed() {
+    Hitable** list = new Hitable*[3];
+    list[0] = new Sphere(vec3(10, 0, 101), 100, new Lambertian(new ConstantTexture(vec3(0.8, 0.8, 0.0))));
+    list[1] = new Sphere(vec3(10, 0, 0), 1, new Lambertian(new ConstantTexture(vec3(0.1, 0.2, 0.5))));
+    list[2] = new Sphere(vec3(10, -2.2, 0), 1, new Lambertian(new ConstantTexture(vec3(0.8, 0.3, 0.3))));
+    return new HitableList(list, 3);
+}
+
+// Config 4: cornellBox_NED() with the smoke box that scenes.h:461-470 keeps
+// commented out, inserted at the position that code occupies (after the
+// rotated box, before the sphere medium).
+static Hitable* cornellSmokeNed() {
+    HitableList* l = dynamic_cast<HitableList*>(cornellBox_NED());
+    Material* green = new Lambertian(new ConstantTexture(vec3(0.12, 0.95, 0.15)));
+    Hitable* box = new Translate(new RotateY(new Box(vec3(0, 0, 0), vec3(160, 300, 160), green), -25),
+                                 vec3(-100, -50, 200));
+    Hitable* smoke = new ConstantMedium(box, 0.01, new ConstantTexture(vec3(0.2, 0.9, 0.4)));
+    const uint32_t at = 9;  // 6 panels + 3 boxes precede it
+    for (uint32_t k = l->_listSize; k > at; k--) l->_hitableList[k] = l->_hitableList[k - 1];
+    l->_hitableList[at] = smoke;
+    l->_listSize += 1;
+    return l;
+}
+
+struct Opts {
+    int n = 100;
+    uint64_t seed = 1;
+    int threads = 0;
+    std::string cwd;
+};
+
+static Hitable* buildWorld(const std::string& name, const Opts& o) {
+    if (!o.cwd.empty() && chdir(o.cwd.c_str()) != 0) { std::perror("chdir"); std::exit(2); }
+    // main.cpp:132 / 136 wrap the scene in a root Translate.
+    if (name == "random_ned") {
+        Hitable* s;
+        if (o.n == 100) {
+            s = randomScene_NED();
+        } else {
+            bool used;
+            s = randomSceneNedN(o.n, &used);
+        }
+        return new Translate(s, vec3(0, 0, 1000));
+    }
+    if (name == "random_ned_restated") {  // for the n = 100 equivalence check only
+        bool used;
+        return new Translate(randomSceneNedN(o.n, &used), vec3(0, 0, 1000));
+    }
+    if (name == "cornell") return new Translate(cornellBox_NED(), vec3(800, 0, 0));
+    if (name == "cornell_smoke") return new Translate(cornellSmokeNed(), vec3(800, 0, 0));
+    if (name == "three_sphere") return threeSphereNed();
+    std::fprintf(stderr, "unknown scene %s\n", name.c_str());
+    std::exit(2);
+}
+
+// main.cpp:111-125
+static Camera* mainCamera(uint32_t W, uint32_t H) {
+    vec3 lookFrom(0, 0, 0), lookAt(1, 0, 0), worldUp(0, 0, -1);
+    float distToFocus = 1000;
+    float aperture = 2.0;
+    float aspectRatio = float(W) / float(H);
+    float vFoV = 60.0;
+    std::streambuf* old = std::cout.rdbuf(nullptr);  // the constructor prints its basis
+    Camera* c = new Camera(lookFrom, lookAt, worldUp, vFoV, aspectRatio, aperture, distToFocus, 0.0, 1.0);
+    std::cout.rdbuf(old);
+    return c;
+}
+
+static void writeCamera(const char* path, Camera* c) {
+    rtow_camera rc{};
+    GraphWriter::v3(rc.origin, c->_origin);
+    GraphWriter::v3(rc.lower_left_corner, c->_lowerLeftCorner);
+    GraphWriter::v3(rc.horizontal, c->_horizontal);
+    GraphWriter::v3(rc.vertical, c->_vertical);
+    GraphWriter::v3(rc.u, c->_u);
+    GraphWriter::v3(rc.v, c->_v);
+    GraphWriter::v3(rc.w, c->_w);
+    rc.lens_radius = c->_lensRadius;
+    rc.time0 = c->_time0;
+    rc.time1 = c->_time1;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) { std::perror(path); std::exit(2); }
+    std::fwrite(&rc, sizeof(rc), 1, f);
+    std::fclose(f);
+}
+
+// main.cpp:932-996, re-stated; thread id / count interleave columns as
+// main.cpp:936 does.  Output in framebuffer order.
+static void renderWorker(int id, int nthreads, Camera* cam, Hitable* world, uint32_t W, uint32_t H,
+                         uint32_t spp, uint64_t seed, float* lin, uint8_t* bgra) {
+    const uint32_t bytesPerPixel = 4;
+    const uint32_t sizeInBytes = W * H * bytesPerPixel;
+    for (int row = (int)H - 1; row >= 0; row--) {
+        for (int i = 0; i < (int)W; i++) {
+            int column = id + nthreads * i;
+            if (column >= (int)W) break;
+            vec3 outputColor(0, 0, 0);
+            for (uint32_t sample = 0; sample < spp; sample++) {
+                CbEngine::key = rtow_sample_key(seed, (uint32_t)row * W + (uint32_t)column, sample);
+                CbEngine::ctr = 0;
+                float u = (float)(column + unifRand(randomNumberGenerator)) / (float)W;
+                float v = (float)(row + unifRand(randomNumberGenerator)) / (float)H;
+                ray rayCast = cam->getRay(u, v);
+                outputColor += color(rayCast, world, 0);
+            }
+            outputColor /= float(spp);
+            uint32_t px = (H - 1 - (uint32_t)row) * W + (uint32_t)column;
+            lin[3 * px + 0] = outputColor[0];
+            lin[3 * px + 1] = outputColor[1];
+            lin[3 * px + 2] = outputColor[2];
+            outputColor = vec3(sqrt(outputColor[0]), sqrt(outputColor[1]), sqrt(outputColor[2]));
+            uint16_t irO = uint16_t(255.99 * outputColor[0]);
+            uint16_t igO = uint16_t(255.99 * outputColor[1]);
+            uint16_t ibO = uint16_t(255.99 * outputColor[2]);
+            uint8_t ir = irO > 255 ? 255 : uint8_t(irO);
+            uint8_t ig = igO > 255 ? 255 : uint8_t(igO);
+            uint8_t ib = ibO > 255 ? 255 : uint8_t(ibO);
+            uint32_t rowIndex = row * W * bytesPerPixel;
+            uint32_t columnIndex = (W * bytesPerPixel) - column * bytesPerPixel;
+            uint32_t bufferIndex = sizeInBytes - (rowIndex + columnIndex);
+            bgra[bufferIndex] = ib;
+            bgra[bufferIndex + 1] = ig;
+            bgra[bufferIndex + 2] = ir;
+            bgra[bufferIndex + 3] = 0;
+        }
+    }
+}
+
+static Opts parseOpts(int argc, char** argv, int first) {
+    Opts o;
+    for (int k = first; k < argc; k++) {
+        std::string a = argv[k];
+        auto next = [&]() -> const char* {
+            if (k + 1 >= argc) { std::fprintf(stderr, "missing value for %s\n", a.c_str()); std::exit(2); }
+            return argv[++k];
+        };
+        if (a == "--n") o.n = std::atoi(next());
+        else if (a == "--seed") o.seed = std::strtoull(next(), nullptr, 0);
+        else if (a == "--threads") o.threads = std::atoi(next());
+        else if (a == "--cwd") o.cwd = next();
+        else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); std::exit(2); }
+    }
+    return o;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: see header\n");
+        return 2;
+    }
+    std::string cmd = argv[1];
+    if (cmd == "dump" && argc >= 4) {
+        Opts o = parseOpts(argc, argv, 4);
+        Hitable* world = buildWorld(argv[2], o);
+        GraphWriter w;
+        uint32_t root = w.hitable(world);
+        w.write(argv[3], root);
+        std::printf("draws %llu hitables %zu\n", (unsigned long long)CbEngine::total, w.hit.size());
+        return 0;
+    }
+    if (cmd == "camera" && argc >= 5) {
+        Camera* c = mainCamera((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]));
+        writeCamera(argv[4], c);
+        return 0;
+    }
+    if (cmd == "render" && argc >= 7) {
+        Opts o = parseOpts(argc, argv, 7);
+        uint32_t W = (uint32_t)std::atoi(argv[3]), H = (uint32_t)std::atoi(argv[4]);
+        uint32_t spp = (uint32_t)std::atoi(argv[5]);
+        std::string prefix = argv[6];
+        Hitable* world = buildWorld(argv[2], o);
+        Camera* cam = mainCamera(W, H);
+        std::vector<float> lin((size_t)W * H * 3, 0.0f);
+        std::vector<uint8_t> bgra((size_t)W * H * 4, 0);
+        int nt = o.threads > 0 ? o.threads : (int)std::thread::hardware_concurrency();
+        std::vector<std::thread> ts;
+        for (int t = 0; t < nt; t++)
+            ts.emplace_back(renderWorker, t, nt, cam, world, W, H, spp, o.seed, lin.data(), bgra.data());
+        for (auto& t : ts) t.join();
+        FILE* f = std::fopen((prefix + ".lin").c_str(), "wb");
+        std::fwrite(lin.data(), 4, lin.size(), f);
+        std::fclose(f);
+        f = std::fopen((prefix + ".bgra").c_str(), "wb");
+        std::fwrite(bgra.data(), 1, bgra.size(), f);
+        std::fclose(f);
+        return 0;
+    }
+    std::fprintf(stderr, "bad command\n");
+    return 2;
+}
