@@ -1,0 +1,1453 @@
+// rtow_device.hip — gfx950 kernels and the device half of the C-ABI.
+//
+// What replaces main.cpp:932-996 (DESIGN.md has the full picture):
+//
+//   trace_kernel   persistent wavefronts.  One lane = one path.  A lane owns a
+//                  work item = (pixel, chunk of consecutive samples); when its
+//                  path ends it starts the next sample, and when its chunk is
+//                  done it writes the chunk sum and takes a new item.  Items are
+//                  handed out per WAVE: __ballot of the lanes that need work,
+//                  one atomicAdd by the leader for popcount(mask) items, and a
+//                  mask-prefix rank per lane -- so live lanes are refilled (the
+//                  "compaction") every bounce without leaving the kernel.
+//                  color() (color.h:12-59) is unrolled into the bounce loop; the
+//                  world->hit recursion (bvhNode.h:66-96, hitableList.h:20-38,
+//                  hitable.h:25-154) is an explicit traversal with a per-lane
+//                  stack in LDS (column-major: conflict-free).
+//   resolve_kernel sums each pixel's chunk sums in order, applies the
+//                  /= float(spp) (vec3.h:133-139), sqrt gamma and the 255.99
+//                  quantisation (main.cpp:955-970) and writes BGRA8 (+ linear).
+//   assemble_kernel scatters rank tile slabs into the framebuffer
+//                  (main.cpp:982-989 layout).
+//
+// Numerics: compiled with -ffp-contract=off and HIP's default correctly
+// rounded f32 division/sqrt, every float expression mirrors the reference's
+// shape (oracle/rtow_oracle.c restates the same expressions on the CPU), and
+// random numbers come from include/rtow_rng.h, keyed per (pixel, sample).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rtow.h"
+#include "../../include/rtow_rng.h"
+#include "rtow_device_layout.h"
+#include "rtow_internal.h"
+
+using namespace rtow_dev;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int MAXCHAIN = 4;
+
+// ---------------------------------------------------------------------------
+// small vector math with the reference's exact operation order (vec3.h)
+struct F3 {
+    float x, y, z;
+};
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ F3 mulv(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ F3 scl(float t, F3 v) { return f3(t * v.x, t * v.y, t * v.z); }
+__device__ __forceinline__ F3 divs(F3 v, float t) { return f3(v.x / t, v.y / t, v.z / t); }
+__device__ __forceinline__ F3 neg(F3 v) { return f3(-v.x, -v.y, -v.z); }
+__device__ __forceinline__ float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float len(F3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+__device__ __forceinline__ float sqlen(F3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+__device__ __forceinline__ F3 unit(F3 v) {
+    float l = len(v);
+    if (l == 0.0f) return f3(0, 0, 0);
+    return divs(v, l);
+}
+__device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]); }
+__device__ __forceinline__ float comp(F3 v, uint32_t i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+struct Ray {
+    F3 o, d;
+    float time;
+};
+__device__ __forceinline__ F3 at(const Ray& r, float t) { return add(r.o, scl(t, r.d)); }
+
+struct Rng {
+    uint64_t key;
+    uint32_t ctr;
+    __device__ __forceinline__ double next() {
+        return (double)rtow_draw24(key, ctr++) * (1.0 / 16777216.0);
+    }
+};
+
+struct DevCam {
+    float origin[3], llc[3], hor[3], ver[3], u[3], v[3];
+    float lens_radius, t0, t1;
+};
+
+struct DevParams {
+    uint32_t width, height, spp, spc;  // spc: samples per chunk
+    uint32_t n_chunks, n_local_px, tiles_x, rank, world;
+    uint32_t max_depth, gi_enable;
+    float sky_gain, gi_gain;
+    uint64_t seed;
+    uint32_t n_items;
+};
+
+struct Chain {
+    uint32_t r[MAXCHAIN];
+    int n;
+};
+
+struct Best {
+    float t;
+    uint32_t prim;
+    Chain ch;
+};
+
+struct Rec {
+    float t, u, v;
+    F3 p, n;
+    uint32_t mat;
+};
+
+// ---------------------------------------------------------------------------
+// instances (hitable.h:53-62, 125-154)
+__device__ __forceinline__ Ray apply_inst(const DevScene& S, uint32_t ref, const Ray& r) {
+    const uint32_t kind = ref >> KIND_SHIFT;
+    const DInst& I = S.inst[ref & INDEX_MASK];
+    Ray q = r;
+    if (kind == DK_TRANSLATE) {
+        q.o = sub(r.o, f3(I.p[0], I.p[1], I.p[2]));
+    } else if (kind == DK_ROTY) {
+        const float s = I.p[0], c = I.p[1];
+        q.o.x = c * r.o.x - s * r.o.z;
+        q.o.z = s * r.o.x + c * r.o.z;
+        q.d.x = c * r.d.x - s * r.d.z;
+        q.d.z = s * r.d.x + c * r.d.z;
+    }
+    return q;
+}
+
+__device__ __forceinline__ Ray chain_ray(const DevScene& S, const Chain& ch, int n, const Ray& w) {
+    Ray r = w;
+#pragma unroll
+    for (int k = 0; k < MAXCHAIN; k++)
+        if (k < n) r = apply_inst(S, ch.r[k], r);
+    return r;
+}
+
+__device__ __forceinline__ F3 inv_dir(F3 d) { return f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+
+// Conservative slab test for culling (never the reference's own AABB::hit,
+// whose divisions only decide WHICH subtrees it visits, not the result).
+__device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, float z0, float z1, const F3& o,
+                                     const F3& inv, float tmin, float tmax, float& tnear) {
+    const float tx0 = (x0 - o.x) * inv.x, tx1 = (x1 - o.x) * inv.x;
+    const float ty0 = (y0 - o.y) * inv.y, ty1 = (y1 - o.y) * inv.y;
+    const float tz0 = (z0 - o.z) * inv.z, tz1 = (z1 - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tf = tf + fabsf(tf) * 4.0e-7f;  // 2*gamma(3) slack: the reference's exact test can pass where ours rounds out
+    tnear = tn;
+    return tn <= tf;
+}
+
+// sphere.h:20-69: returns the root the reference would record, in (tmin, tmax)
+__device__ __forceinline__ bool sphere_t(F3 c, float R, const Ray& r, float tmin, float tmax, float& t) {
+    const F3 oc = sub(r.o, c);
+    const float a = dot(r.d, r.d);
+    const float b = dot(r.d, oc);
+    const float cc = dot(oc, oc) - R * R;
+    const float disc = b * b - a * cc;
+    if (disc > 0) {
+        const float sq = sqrtf(b * b - a * cc);
+        float temp = (-b - sq) / a;
+        if (temp < tmax && temp > tmin) {
+            t = temp;
+            return true;
+        }
+        temp = (-b + sq) / a;
+        if (temp < tmax && temp > tmin) {
+            t = temp;
+            return true;
+        }
+    }
+    return false;
+}
+
+// sphere.h:129-131
+__device__ __forceinline__ F3 msphere_center(const DMSphere& m, float time) {
+    const F3 c0 = ld3(m.c0), c1 = ld3(m.c1);
+    return add(c0, scl((time - m.t0) / (m.t1 - m.t0), sub(c1, c0)));
+}
+
+// sphere.h:93-118 (note: dot(oc, d) here, dot(d, oc) in Sphere::hit -- equal)
+__device__ __forceinline__ bool msphere_t(const DMSphere& m, const Ray& r, float tmin, float tmax, float& t) {
+    const F3 oc = sub(r.o, msphere_center(m, r.time));
+    const float a = dot(r.d, r.d);
+    const float b = dot(oc, r.d);
+    const float c = dot(oc, oc) - m.r * m.r;
+    const float disc = b * b - a * c;
+    if (disc > 0) {
+        const float sq = sqrtf(disc);
+        float temp = (-b - sq) / a;
+        if (temp < tmax && temp > tmin) {
+            t = temp;
+            return true;
+        }
+        temp = (-b + sq) / a;
+        if (temp < tmax && temp > tmin) {
+            t = temp;
+            return true;
+        }
+    }
+    return false;
+}
+
+// xy_rect.h:22-40, 57-75, 92-110 (closed interval: t == tmax is a hit)
+__device__ __forceinline__ void rect_axes(uint32_t axis, uint32_t& i, uint32_t& j, uint32_t& k) {
+    i = axis == 2 ? 1u : 0u;
+    j = axis == 0 ? 1u : 2u;
+    k = axis == 0 ? 2u : (axis == 1 ? 1u : 0u);
+}
+__device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, float t1, float& t) {
+    uint32_t i, j, k;
+    rect_axes(q.axis, i, j, k);
+    const float tt = (q.k - comp(r.o, k)) / comp(r.d, k);
+    if (tt < t0 || tt > t1) return false;
+    const float x = comp(r.o, i) + tt * comp(r.d, i);
+    const float y = comp(r.o, j) + tt * comp(r.d, j);
+    if (x < q.a0 || x > q.a1 || y < q.b0 || y > q.b1) return false;
+    t = tt;
+    return true;
+}
+
+__device__ __forceinline__ void chain_push(Chain& ch, uint32_t ref) {
+#pragma unroll
+    for (int k = 0; k < MAXCHAIN; k++)
+        if (k == ch.n) ch.r[k] = ref;
+    ch.n++;
+}
+
+// ---------------------------------------------------------------------------
+// Closest hit of `root` for a world-space ray, reference semantics.
+// stk: this lane's LDS stack column (entry e at stk[e * BLOCK]).
+template <bool MEDIA, int STACK>
+__device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, float tmin, float tmax, uint32_t* stk,
+                         int sp0, Rng& rng, Best& best, uint32_t& overflow) {
+    Chain ch;
+#pragma unroll
+    for (int k = 0; k < MAXCHAIN; k++) ch.r[k] = 0;
+    ch.n = 0;
+    Ray r = wray;
+    F3 inv = inv_dir(r.d);
+    float bt = tmax;
+    bool found = false;
+    uint32_t cur = root;
+    int sp = sp0;
+    while (true) {
+        const uint32_t kind = cur >> KIND_SHIFT;
+        const uint32_t idx = cur & INDEX_MASK;
+        bool pop = true;
+        if (kind == DK_BVH) {
+            const DBvh& n = S.bvh[idx];
+            const float4 xs = *reinterpret_cast<const float4*>(n.xs);
+            const float4 ys = *reinterpret_cast<const float4*>(n.ys);
+            const float4 zs = *reinterpret_cast<const float4*>(n.zs);
+            const uint2 lr = *reinterpret_cast<const uint2*>(&n.left);
+            float tl, tr;
+            const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, r.o, inv, tmin, bt, tl);
+            const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, r.o, inv, tmin, bt, tr);
+            if (hl && hr) {
+                const bool lfirst = tl <= tr;
+                if (sp < STACK) {
+                    stk[sp * BLOCK] = lfirst ? lr.y : lr.x;
+                    sp++;
+                } else {
+                    overflow = 1;
+                }
+                cur = lfirst ? lr.x : lr.y;
+                pop = false;
+            } else if (hl) {
+                cur = lr.x;
+                pop = false;
+            } else if (hr) {
+                cur = lr.y;
+                pop = false;
+            }
+        } else if (kind == DK_SPHERE) {
+            const float4 cr = *reinterpret_cast<const float4*>(S.sph[idx].c);
+            float t;
+            if (sphere_t(f3(cr.x, cr.y, cr.z), cr.w, r, tmin, bt, t)) {
+                bt = t;
+                best.prim = cur;
+                best.ch = ch;
+                found = true;
+            }
+        } else if (kind == DK_MSPHERE) {
+            float t;
+            if (msphere_t(S.msph[idx], r, tmin, bt, t)) {
+                bt = t;
+                best.prim = cur;
+                best.ch = ch;
+                found = true;
+            }
+        } else if (kind == DK_RECT) {
+            float t;
+            if (rect_t(S.rect[idx], r, tmin, bt, t)) {
+                bt = t;
+                best.prim = cur;
+                best.ch = ch;
+                found = true;
+            }
+        } else if (kind == DK_LIST) {
+            const DList L = S.list[idx];
+            if (L.count > 0) {
+                for (uint32_t k = L.count - 1; k >= 1; k--) {
+                    if (sp < STACK) {
+                        stk[sp * BLOCK] = S.refs[L.first + k];
+                        sp++;
+                    } else {
+                        overflow = 1;
+                    }
+                }
+                cur = S.refs[L.first];
+                pop = false;
+            }
+        } else if (kind == DK_TRANSLATE || kind == DK_ROTY || kind == DK_FLIP) {
+            if (sp < STACK && ch.n < MAXCHAIN) {
+                stk[sp * BLOCK] = mkref(DK_EXIT, 0);
+                sp++;
+                chain_push(ch, cur);
+                r = apply_inst(S, cur, r);
+                inv = inv_dir(r.d);
+                cur = S.inst[idx].child;
+                pop = false;
+            } else {
+                overflow = 1;
+            }
+        } else if (kind == DK_EXIT) {
+            ch.n--;
+            r = chain_ray(S, ch, ch.n, wray);
+            inv = inv_dir(r.d);
+        } else if (kind == DK_MEDIUM) {
+          if constexpr (MEDIA) {
+            // constantMedium.h:26-74, called with the list's current closest
+            // hit as tmax (hitableList.h:30)
+            const DMedium M = S.med[idx];
+            (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
+            Best b1, b2;
+            uint32_t dummy = 0;
+            if (traverse<false, STACK>(S, M.boundary, r, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow)) {
+                const float t1 = b1.t;
+                if (traverse<false, STACK>(S, M.boundary, r, (float)((double)t1 + 0.0001), FLT_MAX, stk, sp, rng, b2,
+                                           overflow)) {
+                    float ta = t1, tb = b2.t;
+                    if (ta < tmin) ta = tmin;
+                    if (tb > bt) tb = bt;
+                    if (!(ta >= tb)) {
+                        if (ta < 0) ta = 0;
+                        const float dl = len(r.d);
+                        const float inside = (tb - ta) * dl;
+                        const float dist = (float)(-(1 / M.density) * log(rng.next()));
+                        if (dist < inside) {
+                            bt = ta + dist / dl;
+                            best.prim = cur;
+                            best.ch = ch;
+                            found = true;
+                        }
+                    }
+                }
+            }
+            (void)dummy;
+          }
+        }
+        if (pop) {
+            if (sp == sp0) break;
+            --sp;
+            cur = stk[sp * BLOCK];
+        }
+    }
+    best.t = bt;
+    return found;
+}
+
+// mathUtilities.h:62-68
+__device__ __forceinline__ void sphere_uv(F3 p, float& u, float& v) {
+    const float phi = atan2f(p.z, p.x);
+    const float theta = asinf(p.y);
+    u = (float)(1 - (phi + M_PI) / (2 * M_PI));
+    v = (float)((theta + M_PI / 2) / M_PI);
+}
+
+// Build the HitRecord of the winning primitive: local ray through the chain,
+// the primitive's record, then the instances' way out, innermost first.
+__device__ void finalize(const DevScene& S, const Best& b, const Ray& wray, Rec& rec) {
+    const Ray r = chain_ray(S, b.ch, b.ch.n, wray);
+    const uint32_t kind = b.prim >> KIND_SHIFT;
+    const uint32_t idx = b.prim & INDEX_MASK;
+    rec.t = b.t;
+    rec.u = 0.0f;
+    rec.v = 0.0f;
+    if (kind == DK_SPHERE) {
+        const DSphere& s = S.sph[idx];
+        const F3 c = ld3(s.c);
+        rec.p = at(r, b.t);
+        rec.n = divs(sub(rec.p, c), s.r);
+        rec.mat = s.mat;
+        if (S.mat[s.mat].needs_uv) sphere_uv(rec.n, rec.u, rec.v);
+    } else if (kind == DK_MSPHERE) {
+        const DMSphere& m = S.msph[idx];
+        rec.p = at(r, b.t);
+        rec.n = divs(sub(rec.p, msphere_center(m, r.time)), m.r);
+        rec.mat = m.mat;
+    } else if (kind == DK_RECT) {
+        const DRect& q = S.rect[idx];
+        uint32_t i, j, k;
+        rect_axes(q.axis, i, j, k);
+        const float x = comp(r.o, i) + b.t * comp(r.d, i);
+        const float y = comp(r.o, j) + b.t * comp(r.d, j);
+        rec.u = (x - q.a0) / (q.a1 - q.a0);
+        rec.v = (y - q.b0) / (q.b1 - q.b0);
+        rec.p = at(r, b.t);
+        rec.n = f3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
+        rec.mat = q.mat;
+    } else {  // DK_MEDIUM
+        const DMedium& m = S.med[idx];
+        rec.p = at(r, b.t);
+        rec.n = f3(1, 0, 0);
+        rec.mat = m.phase_mat;
+    }
+#pragma unroll
+    for (int k = MAXCHAIN - 1; k >= 0; k--) {
+        if (k < b.ch.n) {
+            const uint32_t ref = b.ch.r[k];
+            const uint32_t ik = ref >> KIND_SHIFT;
+            const DInst& I = S.inst[ref & INDEX_MASK];
+            if (ik == DK_FLIP) {
+                rec.n = neg(rec.n);
+            } else if (ik == DK_TRANSLATE) {
+                rec.p = add(rec.p, f3(I.p[0], I.p[1], I.p[2]));
+            } else {
+                const float s = I.p[0], c = I.p[1];
+                F3 p = rec.p, n = rec.n;
+                p.x = c * rec.p.x + s * rec.p.z;
+                p.z = -s * rec.p.x + c * rec.p.z;
+                n.x = c * rec.n.x + s * rec.n.z;
+                n.z = -s * rec.n.x + c * rec.n.z;
+                rec.p = p;
+                rec.n = n;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// textures (texture.h, noise.h, mathUtilities.h:41-60)
+__device__ float perlin_noise(const DevScene& S, F3 p) {
+    const float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
+    const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    const int i = (int)fx, j = (int)fy, k = (int)fz;
+    const float uu = u * u * (3 - 2 * u);
+    const float vv = v * v * (3 - 2 * v);
+    const float ww = w * w * (3 - 2 * w);
+    float accum = 0;
+#pragma unroll
+    for (int di = 0; di < 2; di++)
+#pragma unroll
+        for (int dj = 0; dj < 2; dj++)
+#pragma unroll
+            for (int dk = 0; dk < 2; dk++) {
+                const uint32_t q = (S.perm[(i + di) & 255] & 255u) ^ ((S.perm[(j + dj) & 255] >> 8) & 255u) ^
+                                   ((S.perm[(k + dk) & 255] >> 16) & 255u);
+                const float4 c = *reinterpret_cast<const float4*>(S.ranvec + 4 * q);
+                const F3 wt = f3(u - di, v - dj, w - dk);
+                const float fi = di ? uu : (1 - uu);
+                const float fj = dj ? vv : (1 - vv);
+                const float fk = dk ? ww : (1 - ww);
+                accum += fi * fj * fk * dot(f3(c.x, c.y, c.z), wt);
+            }
+    return accum;
+}
+
+__device__ float turbulence(const DevScene& S, F3 p) {  // noise.h:38-49
+    float accum = 0;
+    F3 tp = p;
+    float weight = 1.0f;
+    for (int i = 0; i < 7; i++) {
+        accum += weight * perlin_noise(S, tp);
+        weight *= 0.5f;
+        tp = scl(2.0f, tp);
+    }
+    return fabsf(accum);
+}
+
+__device__ F3 tex_value(const DevScene& S, uint32_t ti, float u, float v, F3 p) {
+    for (int guard = 0; guard < 32; guard++) {
+        const DTex t = S.tex[ti];
+        if (t.kind == RTOW_TEX_CONSTANT) return f3(t.f[0], t.f[1], t.f[2]);
+        if (t.kind == RTOW_TEX_CHECKER) {  // texture.h:27-35
+            const float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+            ti = sines < 0 ? t.a : t.b;
+            continue;
+        }
+        if (t.kind == RTOW_TEX_NOISE) {  // texture.h:44-48
+            const float s = 1 + sinf(t.f[0] * p.z + 10 * turbulence(S, p));
+            return scl(s, f3(0.5f, 0.5f, 0.5f));
+        }
+        if (t.kind == RTOW_TEX_IMAGE) {  // texture.h:65-79
+            const DImage im = S.img[t.a];
+            const int nx = (int)im.nx, ny = (int)im.ny;
+            const uint8_t* data = S.texels + im.offset;
+            int i = (int)(u * nx);
+            int j = (int)((double)((1 - v) * ny) - 0.001);
+            if (i < 0) i = 0;
+            if (j < 0) j = 0;
+            if (i > nx - 1) i = nx - 1;
+            if (j > ny - 1) j = ny - 1;
+            const size_t o = 3 * (size_t)i + 3 * (size_t)nx * (size_t)j;
+            return f3((float)(data[o] / 255.0), (float)(data[o + 1] / 255.0), (float)(data[o + 2] / 255.0));
+        }
+        break;
+    }
+    return f3(0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// materials (material.h)
+__device__ __forceinline__ F3 random_in_unit_sphere(Rng& g) {  // mathUtilities.h:19-25
+    F3 p;
+    do {
+        const double c = g.next();  // g++ evaluates vec3(U, U, U) right to left
+        const double b = g.next();
+        const double a = g.next();
+        p = sub(scl(2.0f, f3((float)a, (float)b, (float)c)), f3(1, 1, 1));
+    } while (sqlen(p) >= 1.0f);
+    return p;
+}
+
+__device__ __forceinline__ F3 reflect(F3 v, F3 n) { return sub(v, scl(2 * dot(v, n), n)); }
+
+__device__ __forceinline__ bool refract(F3 d, F3 n, float ni, F3& out) {  // material.h:15-26
+    const F3 uv = unit(d);
+    const float dt = dot(uv, n);
+    const float disc = (float)(1.0 - ni * ni * (1 - dt * dt));
+    if (disc > 0) {
+        out = sub(scl(ni, sub(uv, scl(dt, n))), scl(sqrtf(disc), n));
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ float schlick(float cosine, float ri) {  // material.h:28-32
+    float r0 = (1 - ri) / (1 + ri);
+    r0 = r0 * r0;
+    return (float)(r0 + (1 - r0) * pow((double)(1 - cosine), 5.0));
+}
+
+__device__ bool scatter(const DevScene& S, const DMat& m, const Ray& in, const Rec& rec, Rng& g, F3& atten,
+                        Ray& out) {
+    switch (m.kind) {
+    case RTOW_MAT_LAMBERTIAN: {  // material.h:47-53
+        const F3 target = add(add(rec.p, rec.n), random_in_unit_sphere(g));
+        out.o = rec.p;
+        out.d = sub(target, rec.p);
+        out.time = in.time;
+        atten = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        return true;
+    }
+    case RTOW_MAT_METAL: {  // material.h:62-67
+        const F3 reflected = reflect(unit(in.d), rec.n);
+        out.o = rec.p;
+        out.d = add(reflected, scl(m.param, random_in_unit_sphere(g)));
+        out.time = 0.0f;
+        atten = ld3(m.albedo);
+        return dot(out.d, rec.n) > 0;
+    }
+    case RTOW_MAT_DIELECTRIC: {  // material.h:77-117
+        const float ri = m.param;
+        const F3 reflected = reflect(in.d, rec.n);
+        F3 outward, refracted = f3(0, 0, 0);
+        float ni, cosine, prob;
+        atten = f3(1.0f, 1.0f, 1.0f);
+        const float dn = dot(in.d, rec.n);
+        if (dn > 0) {
+            outward = neg(rec.n);
+            ni = ri;
+            cosine = ri * dot(in.d, rec.n) / len(in.d);
+        } else {
+            outward = rec.n;
+            ni = (float)(1.0 / ri);
+            cosine = -dot(in.d, rec.n) / len(in.d);
+        }
+        if (refract(in.d, outward, ni, refracted))
+            prob = schlick(cosine, ri);
+        else
+            prob = 1.0f;
+        out.o = rec.p;
+        out.time = 0.0f;
+        out.d = (g.next() < prob) ? reflected : refracted;
+        return true;
+    }
+    case RTOW_MAT_ISOTROPIC: {  // material.h:141-145
+        out.o = rec.p;
+        out.d = random_in_unit_sphere(g);
+        out.time = 0.0f;
+        atten = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        return true;
+    }
+    default:  // DiffuseLight never scatters (material.h:126-128)
+        return false;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// work-item decoding: item = chunk * n_local_px + local pixel; a local pixel
+// is (slot of this rank's tile, position in the 8x8 tile)
+__device__ __forceinline__ bool decode_pixel(const DevParams& P, uint32_t lp, uint32_t& x, uint32_t& yimg) {
+    const uint32_t slot = lp >> 6, q = lp & 63;
+    const uint32_t tile = P.rank + slot * P.world;
+    x = (tile % P.tiles_x) * 8 + (q & 7);
+    yimg = (tile / P.tiles_x) * 8 + (q >> 3);
+    return x < P.width && yimg < P.height;
+}
+
+template <bool MEDIA, int STACK>
+__global__ __launch_bounds__(BLOCK) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
+                                                       float4* partial, unsigned long long* counters) {
+    __shared__ uint32_t s_stack[STACK * BLOCK];
+    uint32_t* stk = s_stack + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+
+    uint32_t item = 0, s = 0, s_end = 0, pixkey = 0, depth = 0, nseg = 0, overflow = 0;
+    uint32_t col = 0, row = 0;
+    bool need_item = true, need_sample = false;
+    F3 acc = f3(0, 0, 0), thr = f3(1, 1, 1);
+    Ray ray;
+    ray.o = f3(0, 0, 0);
+    ray.d = f3(0, 0, 1);
+    ray.time = 0;
+    Rng rng{0, 0};
+
+    while (true) {
+        // ---- wave-wide refill of lanes whose work item is finished ----
+        const unsigned long long want = __ballot(need_item);
+        if (want) {
+            const uint32_t cnt = (uint32_t)__popcll(want);
+            const uint32_t leader = (uint32_t)__ffsll((long long)want) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(work, cnt);
+            base = __shfl(base, (int)leader);
+            if (need_item) {
+                const uint32_t rank = (uint32_t)__popcll(want & ((1ull << lane) - 1ull));
+                item = base + rank;
+                if (item >= P.n_items) break;
+                const uint32_t chunk = item / P.n_local_px;
+                const uint32_t lp = item - chunk * P.n_local_px;
+                uint32_t x, yimg;
+                if (!decode_pixel(P, lp, x, yimg)) continue;  // padding pixel of a partial tile
+                col = x;
+                row = P.height - 1u - yimg;  // reference row numbering (main.cpp:932)
+                pixkey = row * P.width + col;
+                s = chunk * P.spc;
+                s_end = min(s + P.spc, P.spp);
+                acc = f3(0, 0, 0);
+                need_item = false;
+                need_sample = true;
+            }
+        }
+        if (need_sample) {
+            // main.cpp:943-946 + camera.h:123-135 (CAMERA_DOF_EN 0)
+            rng.key = rtow_sample_key(P.seed, pixkey, s);
+            rng.ctr = 0;
+            const float u = (float)((double)col + rng.next()) / (float)P.width;
+            const float v = (float)((double)row + rng.next()) / (float)P.height;
+            const F3 rd = scl(C.lens_radius, f3(1.0f, 1.0f, 1.0f));
+            const F3 offset = add(scl(rd.x, ld3(C.u)), scl(rd.y, ld3(C.v)));
+            const float time = (float)((double)C.t0 + rng.next() * (double)(C.t1 - C.t0));
+            ray.o = add(ld3(C.origin), offset);
+            ray.d = sub(sub(add(add(ld3(C.llc), scl(u, ld3(C.hor))), scl(v, ld3(C.ver))), ld3(C.origin)), offset);
+            ray.time = time;
+            thr = f3(1, 1, 1);
+            depth = 0;
+            need_sample = false;
+        }
+
+        // ---- one segment = one color() call (color.h:12-59) ----
+        nseg++;
+        Best best;
+        best.prim = 0;
+        best.ch.n = 0;
+        const bool hit = traverse<MEDIA, STACK>(S, S.root, ray, 0.001f, FLT_MAX, stk, 0, rng, best, overflow);
+        bool done = true;
+        F3 contrib = f3(0, 0, 0);
+        if (hit) {
+            Rec rec;
+            finalize(S, best, ray, rec);
+            const DMat m = S.mat[rec.mat];
+            Ray sc;
+            F3 att;
+            if (depth < P.max_depth && scatter(S, m, ray, rec, rng, att, sc)) {
+                // emitted() is (0,0,0) for every material that scatters
+                // (material.h:38-40; DiffuseLight never scatters), so the
+                // recursion's `emitted + attenuation * color(...)` is a product
+                thr = mulv(thr, att);
+                ray = sc;
+                depth++;
+                done = false;
+            } else if (m.kind == RTOW_MAT_DIFFUSE_LIGHT) {
+                contrib = mulv(thr, tex_value(S, m.tex, rec.u, rec.v, rec.p));
+            }
+        } else if (P.gi_enable) {
+            if (depth < 1) {  // color.h:35-50
+                const F3 ud = unit(ray.d);
+                const float t = ud.z;
+                const float rt = (float)(1.0 + t);
+                const F3 sky = f3((float)(rt * 0.1), (float)(rt * 0.3), (float)(rt * 1.0));
+                contrib = mulv(thr, scl(P.sky_gain, sky));
+            } else {
+                contrib = mulv(thr, f3(P.gi_gain, P.gi_gain, P.gi_gain));
+            }
+        }
+        if (done) {
+            acc = add(acc, contrib);
+            s++;
+            if (s >= s_end) {
+                partial[item] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+                need_item = true;
+            } else {
+                need_sample = true;
+            }
+        }
+    }
+
+    // ---- per-wave counter reduction, one atomic per wave ----
+    uint32_t v = nseg;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const unsigned long long ov = __ballot(overflow != 0);
+    if (lane == 0) {
+        atomicAdd(&counters[0], (unsigned long long)v);
+        if (ov) atomicAdd(&counters[1], 1ull);
+    }
+}
+
+__global__ void resolve_kernel(DevParams P, const float4* partial, uint8_t* slab_bgra, float* slab_lin,
+                               uint8_t* fb_bgra, float* fb_lin) {
+    const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= P.n_local_px) return;
+    uint32_t x, yimg;
+    const bool valid = decode_pixel(P, lp, x, yimg);
+    if (!valid) {
+        if (slab_bgra) *reinterpret_cast<uint32_t*>(slab_bgra + 4 * (size_t)lp) = 0u;
+        if (slab_lin) {
+            slab_lin[3 * (size_t)lp] = 0.0f;
+            slab_lin[3 * (size_t)lp + 1] = 0.0f;
+            slab_lin[3 * (size_t)lp + 2] = 0.0f;
+        }
+        return;
+    }
+    float4 a = partial[lp];
+    F3 acc = f3(a.x, a.y, a.z);
+    for (uint32_t c = 1; c < P.n_chunks; c++) {
+        const float4 b = partial[(size_t)c * P.n_local_px + lp];
+        acc = add(acc, f3(b.x, b.y, b.z));
+    }
+    const float k = (float)(1.0 / (double)(float)P.spp);  // vec3.h:133-139
+    const F3 lin = f3(acc.x * k, acc.y * k, acc.z * k);
+    const float sq[3] = {sqrtf(lin.x), sqrtf(lin.y), sqrtf(lin.z)};
+    uint32_t q[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {  // main.cpp:961-970
+        const double d = 255.99 * (double)sq[i];
+        const uint32_t u16 = d >= 65535.0 ? 65535u : (d > 0.0 ? (uint32_t)d : 0u);
+        q[i] = u16 > 255u ? 255u : u16;
+    }
+    const uint32_t px = q[2] | (q[1] << 8) | (q[0] << 16);  // B, G, R, alpha 0 (main.cpp:982-989)
+    if (slab_bgra) *reinterpret_cast<uint32_t*>(slab_bgra + 4 * (size_t)lp) = px;
+    if (slab_lin) {
+        slab_lin[3 * (size_t)lp] = lin.x;
+        slab_lin[3 * (size_t)lp + 1] = lin.y;
+        slab_lin[3 * (size_t)lp + 2] = lin.z;
+    }
+    const size_t fb = (size_t)yimg * P.width + x;
+    if (fb_bgra) *reinterpret_cast<uint32_t*>(fb_bgra + 4 * fb) = px;
+    if (fb_lin) {
+        fb_lin[3 * fb] = lin.x;
+        fb_lin[3 * fb + 1] = lin.y;
+        fb_lin[3 * fb + 2] = lin.z;
+    }
+}
+
+__global__ void assemble_kernel(uint32_t W, uint32_t H, uint32_t world, uint32_t tiles_x, const uint32_t* slabs,
+                                uint32_t stride_px, uint32_t* fb) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W * H) return;
+    const uint32_t x = i % W, y = i / W;
+    const uint32_t tile = (y >> 3) * tiles_x + (x >> 3);
+    const uint32_t rank = tile % world, slot = tile / world;
+    fb[i] = slabs[(size_t)rank * stride_px + slot * 64u + (y & 7u) * 8u + (x & 7u)];
+}
+
+}  // namespace
+
+// ===========================================================================
+// host side: scene conversion, context, C-ABI
+// ===========================================================================
+
+#define HIP_TRY(expr)                                                                               \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess)                                                                       \
+            return set_error(RTOW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));        \
+    } while (0)
+
+namespace {
+
+struct HostLayout {
+    std::vector<DBvh> bvh;
+    std::vector<DSphere> sph;
+    std::vector<DMSphere> msph;
+    std::vector<DRect> rect;
+    std::vector<DInst> inst;
+    std::vector<DList> list;
+    std::vector<uint32_t> refs;
+    std::vector<DMedium> med;
+    std::vector<DMat> mat;
+    std::vector<DTex> tex;
+    std::vector<float> ranvec;
+    std::vector<uint32_t> perm;
+    std::vector<DImage> img;
+    std::vector<uint8_t> texels;
+    uint32_t root = 0;
+    uint32_t stack_need = 0;
+    uint32_t chain_need = 0;
+    bool has_media = false;
+};
+
+struct Converter {
+    const rtow_scene& s;
+    HostLayout& L;
+    std::unordered_map<uint32_t, uint32_t> memo;
+    std::string err;
+    int depth = 0;
+
+    bool boxOf(uint32_t hi, float* mn, float* mx) {
+        // exact reference bounding boxes where the kernel may cull with them
+        const rtow_hitable& h = s.hitables[hi];
+        switch (h.kind) {
+        case RTOW_HIT_BVH_NODE:
+            for (int a = 0; a < 3; a++) {
+                mn[a] = h.f[a];
+                mx[a] = h.f[3 + a];
+            }
+            return true;
+        case RTOW_HIT_SPHERE:
+            for (int a = 0; a < 3; a++) {
+                mn[a] = h.f[a] - h.f[3];
+                mx[a] = h.f[a] + h.f[3];
+            }
+            return true;
+        case RTOW_HIT_MOVING_SPHERE: {
+            const float r = h.f[8];
+            for (int a = 0; a < 3; a++) {
+                // center(t0) = c0, center(t1) = c1 up to rounding; pad by the radius
+                float lo = std::min(h.f[a], h.f[3 + a]), hi2 = std::max(h.f[a], h.f[3 + a]);
+                mn[a] = lo - r;
+                mx[a] = hi2 + r;
+            }
+            return true;
+        }
+        default:
+            for (int a = 0; a < 3; a++) {
+                mn[a] = -FLT_MAX;
+                mx[a] = FLT_MAX;
+            }
+            return true;
+        }
+    }
+
+    uint32_t conv(uint32_t hi, bool underBvh) {
+        auto it = memo.find(hi);
+        if (it != memo.end()) return it->second;
+        if (hi >= s.n_hitables || ++depth > 4096) {
+            err = "bad hitable index or cyclic scene";
+            return mkref(DK_NONE, 0);
+        }
+        const rtow_hitable& h = s.hitables[hi];
+        uint32_t ref = mkref(DK_NONE, 0);
+        switch (h.kind) {
+        case RTOW_HIT_SPHERE: {
+            DSphere d{};
+            for (int a = 0; a < 3; a++) d.c[a] = h.f[a];
+            d.r = h.f[3];
+            d.mat = h.a;
+            ref = mkref(DK_SPHERE, (uint32_t)L.sph.size());
+            L.sph.push_back(d);
+            break;
+        }
+        case RTOW_HIT_MOVING_SPHERE: {
+            DMSphere d{};
+            for (int a = 0; a < 3; a++) {
+                d.c0[a] = h.f[a];
+                d.c1[a] = h.f[3 + a];
+            }
+            d.t0 = h.f[6];
+            d.t1 = h.f[7];
+            d.r = h.f[8];
+            d.mat = h.a;
+            ref = mkref(DK_MSPHERE, (uint32_t)L.msph.size());
+            L.msph.push_back(d);
+            break;
+        }
+        case RTOW_HIT_RECT_XY:
+        case RTOW_HIT_RECT_XZ:
+        case RTOW_HIT_RECT_YZ: {
+            DRect d{};
+            d.a0 = h.f[0];
+            d.a1 = h.f[1];
+            d.b0 = h.f[2];
+            d.b1 = h.f[3];
+            d.k = h.f[4];
+            d.axis = h.kind == RTOW_HIT_RECT_XY ? 0u : (h.kind == RTOW_HIT_RECT_XZ ? 1u : 2u);
+            d.mat = h.a;
+            ref = mkref(DK_RECT, (uint32_t)L.rect.size());
+            L.rect.push_back(d);
+            break;
+        }
+        case RTOW_HIT_FLIP_NORMALS:
+        case RTOW_HIT_TRANSLATE:
+        case RTOW_HIT_ROTATE_Y: {
+            uint32_t k = h.kind == RTOW_HIT_FLIP_NORMALS ? DK_FLIP : (h.kind == RTOW_HIT_TRANSLATE ? DK_TRANSLATE : DK_ROTY);
+            uint32_t slot = (uint32_t)L.inst.size();
+            L.inst.push_back(DInst{});
+            ref = mkref(k, slot);
+            memo[hi] = ref;
+            uint32_t child = conv(h.a, underBvh);
+            DInst d{};
+            d.child = child;
+            for (int a = 0; a < 6; a++) d.p[a] = (k == DK_ROTY && a >= 2) ? 0.0f : h.f[a];
+            L.inst[slot] = d;
+            break;
+        }
+        case RTOW_HIT_LIST: {
+            uint32_t slot = (uint32_t)L.list.size();
+            L.list.push_back(DList{});
+            ref = mkref(DK_LIST, slot);
+            memo[hi] = ref;
+            uint32_t first = (uint32_t)L.refs.size();
+            L.refs.resize(L.refs.size() + h.b);
+            for (uint32_t i = 0; i < h.b; i++) {
+                uint32_t c = conv(s.refs[h.a + i], underBvh);
+                L.refs[first + i] = c;
+            }
+            L.list[slot] = DList{first, h.b, 0, 0};
+            break;
+        }
+        case RTOW_HIT_BOX:
+            ref = conv(h.a, underBvh);
+            break;
+        case RTOW_HIT_BVH_NODE: {
+            if (h.a == h.b) {  // n == 1 node: both children are the same leaf
+                ref = conv(h.a, true);
+                break;
+            }
+            uint32_t slot = (uint32_t)L.bvh.size();
+            L.bvh.push_back(DBvh{});
+            ref = mkref(DK_BVH, slot);
+            memo[hi] = ref;
+            uint32_t l = conv(h.a, true), r = conv(h.b, true);
+            DBvh d{};
+            float lmn[3], lmx[3], rmn[3], rmx[3];
+            boxOf(h.a, lmn, lmx);
+            boxOf(h.b, rmn, rmx);
+            d.xs[0] = lmn[0]; d.xs[1] = lmx[0]; d.xs[2] = rmn[0]; d.xs[3] = rmx[0];
+            d.ys[0] = lmn[1]; d.ys[1] = lmx[1]; d.ys[2] = rmn[1]; d.ys[3] = rmx[1];
+            d.zs[0] = lmn[2]; d.zs[1] = lmx[2]; d.zs[2] = rmn[2]; d.zs[3] = rmx[2];
+            d.left = l;
+            d.right = r;
+            L.bvh[slot] = d;
+            break;
+        }
+        case RTOW_HIT_CONSTANT_MEDIUM: {
+            if (underBvh) {
+                err = "ConstantMedium below a BvhNode: its random draws follow the reference's exhaustive "
+                      "BVH visit order, which the device traversal does not reproduce";
+                return mkref(DK_NONE, 0);
+            }
+            L.has_media = true;
+            uint32_t slot = (uint32_t)L.med.size();
+            L.med.push_back(DMedium{});
+            ref = mkref(DK_MEDIUM, slot);
+            memo[hi] = ref;
+            uint32_t b = conv(h.a, underBvh);
+            L.med[slot] = DMedium{b, h.b, h.f[0], 0};
+            break;
+        }
+        default:
+            err = "unknown hitable kind";
+            return mkref(DK_NONE, 0);
+        }
+        memo[hi] = ref;
+        depth--;
+        return ref;
+    }
+};
+
+// Upper bound on the traversal stack (entries) and instance nesting a ray
+// can need below `ref`; media add their boundary's sub-traversal.
+struct Bounds {
+    const HostLayout& L;
+    std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> memo;
+    bool mediaInBoundary = false;
+    std::pair<uint32_t, uint32_t> need(uint32_t ref, bool inMedium) {
+        auto it = memo.find(ref);
+        if (it != memo.end() && !inMedium) return it->second;
+        const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+        std::pair<uint32_t, uint32_t> r{0, 0};
+        switch (kind) {
+        case DK_BVH: {
+            auto a = need(L.bvh[idx].left, inMedium), b = need(L.bvh[idx].right, inMedium);
+            r = {1 + std::max(a.first, b.first), std::max(a.second, b.second)};
+            break;
+        }
+        case DK_LIST: {
+            const DList& l = L.list[idx];
+            for (uint32_t i = 0; i < l.count; i++) {
+                auto c = need(L.refs[l.first + i], inMedium);
+                r.first = std::max(r.first, (l.count - 1 - i) + c.first);
+                r.second = std::max(r.second, c.second);
+            }
+            break;
+        }
+        case DK_TRANSLATE:
+        case DK_ROTY:
+        case DK_FLIP: {
+            auto c = need(L.inst[idx].child, inMedium);
+            r = {1 + c.first, 1 + c.second};
+            break;
+        }
+        case DK_MEDIUM: {
+            if (inMedium) mediaInBoundary = true;
+            auto c = need(L.med[idx].boundary, true);
+            r = c;
+            break;
+        }
+        default:
+            break;
+        }
+        if (!inMedium) memo[ref] = r;
+        return r;
+    }
+};
+
+bool textureNeedsUv(const rtow_scene& s, uint32_t ti, int guard = 0) {
+    if (ti >= s.n_textures || guard > 32) return false;
+    const rtow_texture& t = s.textures[ti];
+    if (t.kind == RTOW_TEX_IMAGE) return true;
+    if (t.kind == RTOW_TEX_CHECKER) return textureNeedsUv(s, t.a, guard + 1) || textureNeedsUv(s, t.b, guard + 1);
+    return false;
+}
+
+int buildLayout(const rtow_scene& s, HostLayout& L) {
+    if (s.root >= s.n_hitables || !s.hitables || !s.materials || !s.textures || !s.perlin)
+        return set_error(RTOW_E_INVALID, "incomplete scene");
+    for (uint32_t i = 0; i < s.n_hitables; i++) {
+        const rtow_hitable& h = s.hitables[i];
+        if ((h.kind == RTOW_HIT_SPHERE || h.kind == RTOW_HIT_MOVING_SPHERE || h.kind == RTOW_HIT_RECT_XY ||
+             h.kind == RTOW_HIT_RECT_XZ || h.kind == RTOW_HIT_RECT_YZ) &&
+            h.a >= s.n_materials)
+            return set_error(RTOW_E_INVALID, "material index out of range");
+        if (h.kind == RTOW_HIT_LIST && (uint64_t)h.a + h.b > s.n_refs)
+            return set_error(RTOW_E_INVALID, "list range out of range");
+        if (h.kind == RTOW_HIT_CONSTANT_MEDIUM && h.b >= s.n_materials)
+            return set_error(RTOW_E_INVALID, "phase material out of range");
+    }
+    Converter cv{s, L};
+    L.root = cv.conv(s.root, false);
+    if (!cv.err.empty()) return set_error(RTOW_E_UNSUPPORTED, cv.err);
+    Bounds bd{L};
+    auto nb = bd.need(L.root, false);
+    if (bd.mediaInBoundary) return set_error(RTOW_E_UNSUPPORTED, "ConstantMedium inside a medium boundary");
+    L.stack_need = nb.first;
+    L.chain_need = nb.second;
+    if (L.chain_need > (uint32_t)MAXCHAIN)
+        return set_error(RTOW_E_UNSUPPORTED, "instance nesting deeper than " + std::to_string(MAXCHAIN));
+    for (uint32_t i = 0; i < s.n_materials; i++) {
+        const rtow_material& m = s.materials[i];
+        DMat d{};
+        d.kind = m.kind;
+        d.tex = m.texture;
+        d.param = m.param;
+        for (int a = 0; a < 3; a++) d.albedo[a] = m.albedo[a];
+        if ((m.kind == RTOW_MAT_LAMBERTIAN || m.kind == RTOW_MAT_DIFFUSE_LIGHT || m.kind == RTOW_MAT_ISOTROPIC) &&
+            m.texture >= s.n_textures)
+            return set_error(RTOW_E_INVALID, "texture index out of range");
+        d.needs_uv = (m.kind == RTOW_MAT_METAL || m.kind == RTOW_MAT_DIELECTRIC) ? 0u
+                                                                                 : (textureNeedsUv(s, m.texture) ? 1u : 0u);
+        L.mat.push_back(d);
+    }
+    for (uint32_t i = 0; i < s.n_textures; i++) {
+        DTex d{};
+        std::memcpy(&d, &s.textures[i], sizeof d);
+        if (d.kind == RTOW_TEX_IMAGE && d.a >= s.n_images) return set_error(RTOW_E_INVALID, "image index out of range");
+        if (d.kind == RTOW_TEX_CHECKER && (d.a >= s.n_textures || d.b >= s.n_textures))
+            return set_error(RTOW_E_INVALID, "checker child out of range");
+        L.tex.push_back(d);
+    }
+    L.ranvec.resize(256 * 4);
+    L.perm.resize(256);
+    for (int i = 0; i < 256; i++) {
+        for (int a = 0; a < 3; a++) L.ranvec[4 * i + a] = s.perlin->ranvec[i][a];
+        L.ranvec[4 * i + 3] = 0.0f;
+        L.perm[i] = ((uint32_t)s.perlin->perm_x[i] & 255u) | (((uint32_t)s.perlin->perm_y[i] & 255u) << 8) |
+                    (((uint32_t)s.perlin->perm_z[i] & 255u) << 16);
+    }
+    for (uint32_t i = 0; i < s.n_images; i++) {
+        const rtow_image& im = s.images[i];
+        if (im.channels != 3 || im.offset + (uint64_t)im.nx * im.ny * 3 > s.n_texel_bytes)
+            return set_error(RTOW_E_INVALID, "image outside texel buffer (RGB8 expected)");
+        L.img.push_back(DImage{im.nx, im.ny, im.offset});
+    }
+    if (s.n_texel_bytes) L.texels.assign(s.texels, s.texels + s.n_texel_bytes);
+    // keep every array non-empty so each gets a valid device pointer
+    if (L.bvh.empty()) L.bvh.push_back(DBvh{});
+    if (L.sph.empty()) L.sph.push_back(DSphere{});
+    if (L.msph.empty()) L.msph.push_back(DMSphere{});
+    if (L.rect.empty()) L.rect.push_back(DRect{});
+    if (L.inst.empty()) L.inst.push_back(DInst{});
+    if (L.list.empty()) L.list.push_back(DList{});
+    if (L.refs.empty()) L.refs.push_back(0);
+    if (L.med.empty()) L.med.push_back(DMedium{});
+    if (L.img.empty()) L.img.push_back(DImage{});
+    if (L.texels.empty()) L.texels.push_back(0);
+    return RTOW_OK;
+}
+
+}  // namespace
+
+struct rtow_context {
+    int device = 0;
+    int cus = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    // scene
+    void* d_scene = nullptr;
+    DevScene scene{};
+    bool has_scene = false;
+    // work buffers
+    void* d_work = nullptr;  // [0] work counter (u32) | [8..] u64 counters
+    float4* d_partial = nullptr;
+    size_t partial_bytes = 0;
+    uint8_t* d_fb = nullptr;  // rtow_render: BGRA frame + linear frame
+    size_t fb_bytes = 0;
+};
+
+namespace {
+
+template <class T>
+size_t pushBlob(std::vector<uint8_t>& blob, const std::vector<T>& v) {
+    size_t off = (blob.size() + 255) & ~size_t(255);
+    blob.resize(off + v.size() * sizeof(T));
+    std::memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+int ensure(void** p, size_t* have, size_t need) {
+    if (*have >= need) return RTOW_OK;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *have = 0;
+    HIP_TRY(hipMalloc(p, need));
+    *have = need;
+    return RTOW_OK;
+}
+
+template <bool MEDIA, int STACK>
+int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+    int occ = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MEDIA, STACK>, BLOCK, 0));
+    if (occ < 1) occ = 1;
+    uint32_t per = bpc ? bpc : (uint32_t)occ;
+    uint32_t grid = (uint32_t)c->cus * per;
+    uint32_t maxUseful = (P.n_items + BLOCK - 1) / BLOCK;
+    if (grid > maxUseful) grid = std::max(1u, maxUseful);
+    hipLaunchKernelGGL((trace_kernel<MEDIA, STACK>), dim3(grid), dim3(BLOCK), 0, st, c->scene, cam, P,
+                       (uint32_t*)c->d_work, c->d_partial, (unsigned long long*)((uint8_t*)c->d_work + 8));
+    HIP_TRY(hipGetLastError());
+    return RTOW_OK;
+}
+
+int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+    const uint32_t need = c->scene.stack_need;
+    const bool media = c->scene.has_media != 0;
+    if (need <= 16) return media ? launchTrace<true, 16>(c, cam, P, bpc, st) : launchTrace<false, 16>(c, cam, P, bpc, st);
+    if (need <= 32) return media ? launchTrace<true, 32>(c, cam, P, bpc, st) : launchTrace<false, 32>(c, cam, P, bpc, st);
+    if (need <= 64) return media ? launchTrace<true, 64>(c, cam, P, bpc, st) : launchTrace<false, 64>(c, cam, P, bpc, st);
+    return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
+}
+
+int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
+    if (!p || p->width == 0 || p->height == 0 || p->spp == 0) return set_error(RTOW_E_INVALID, "bad params");
+    if ((uint64_t)p->width * p->height > (1ull << 31)) return set_error(RTOW_E_INVALID, "image too large");
+    uint32_t world = p->world ? p->world : 1;
+    if (p->rank >= world) return set_error(RTOW_E_INVALID, "rank >= world");
+    std::memset(&P, 0, sizeof P);
+    P.width = p->width;
+    P.height = p->height;
+    P.spp = p->spp;
+    uint32_t spc = p->samples_per_chunk ? p->samples_per_chunk : 64;
+    if (spc > p->spp) spc = p->spp;
+    P.n_chunks = (p->spp + spc - 1) / spc;
+    if (P.n_chunks > 256 && !p->samples_per_chunk) {
+        spc = (p->spp + 255) / 256;
+        P.n_chunks = (p->spp + spc - 1) / spc;
+    }
+    P.spc = spc;
+    P.tiles_x = (p->width + 7) / 8;
+    P.rank = p->rank;
+    P.world = world;
+    P.n_local_px = rtow_rank_tile_count(p->width, p->height, p->rank, world) * 64u;
+    uint64_t items = (uint64_t)P.n_chunks * P.n_local_px;
+    if (items >= (1ull << 32) - (1ull << 20)) return set_error(RTOW_E_INVALID, "too many work items; raise samples_per_chunk");
+    P.n_items = (uint32_t)items;
+    P.max_depth = p->max_depth;
+    P.gi_enable = p->gi_enable;
+    P.sky_gain = p->sky_gain;
+    P.gi_gain = p->gi_gain;
+    P.seed = p->seed;
+    (void)c;
+    return RTOW_OK;
+}
+
+DevCam makeCam(const rtow_camera* cam) {
+    DevCam d{};
+    for (int a = 0; a < 3; a++) {
+        d.origin[a] = cam->origin[a];
+        d.llc[a] = cam->lower_left_corner[a];
+        d.hor[a] = cam->horizontal[a];
+        d.ver[a] = cam->vertical[a];
+        d.u[a] = cam->u[a];
+        d.v[a] = cam->v[a];
+    }
+    d.lens_radius = cam->lens_radius;
+    d.t0 = cam->time0;
+    d.t1 = cam->time1;
+    return d;
+}
+
+// trace + resolve on `st`; outputs may be NULL
+int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, uint8_t* slab_bgra, float* slab_lin,
+               uint8_t* fb_bgra, float* fb_lin, hipStream_t st, rtow_stats* stats) {
+    auto t0 = std::chrono::steady_clock::now();
+    if (!c || !cam) return set_error(RTOW_E_INVALID, "NULL context or camera");
+    if (!c->has_scene) return set_error(RTOW_E_INVALID, "no scene uploaded");
+    DevParams P;
+    int rc = makeParams(c, p, P);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    size_t need = (size_t)P.n_chunks * P.n_local_px * sizeof(float4);
+    rc = ensure((void**)&c->d_partial, &c->partial_bytes, std::max<size_t>(need, 16));
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_work, 0, 64, st));
+    const DevCam dc = makeCam(cam);
+    HIP_TRY(hipEventRecord(c->ev[0], st));
+    if (P.n_items) {
+        rc = dispatchTrace(c, dc, P, p->blocks_per_cu, st);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipEventRecord(c->ev[1], st));
+    if (P.n_local_px) {
+        hipLaunchKernelGGL(resolve_kernel, dim3((P.n_local_px + 255) / 256), dim3(256), 0, st, P, c->d_partial, slab_bgra,
+                           slab_lin, fb_bgra, fb_lin);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev[2], st));
+    unsigned long long host_ctr[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(host_ctr, (uint8_t*)c->d_work + 8, 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
+    if (stats) {
+        float k = 0, r = 0;
+        HIP_TRY(hipEventElapsedTime(&k, c->ev[0], c->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&r, c->ev[1], c->ev[2]));
+        uint64_t valid = 0;
+        {
+            // count valid pixels of this rank
+            uint32_t ntile = rtow_rank_tile_count(P.width, P.height, P.rank, P.world);
+            for (uint32_t sl = 0; sl < ntile; sl++) {
+                uint32_t tile = P.rank + sl * P.world;
+                uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+                uint32_t w = std::min(8u, P.width - tx * 8), h = std::min(8u, P.height - ty * 8);
+                valid += (uint64_t)w * h;
+            }
+        }
+        stats->segments = host_ctr[0];
+        stats->pixels = valid;
+        stats->samples = valid * P.spp;
+        stats->kernel_ms = k;
+        stats->resolve_ms = r;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return RTOW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtow_device_count(int* count) {
+    if (!count) return set_error(RTOW_E_INVALID, "NULL count");
+    *count = 0;
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) {
+        *count = 0;
+        return set_error(RTOW_E_NO_DEVICE, hipGetErrorString(e));
+    }
+    return RTOW_OK;
+}
+
+int rtow_context_create(int device, rtow_context** out) {
+    if (!out) return set_error(RTOW_E_INVALID, "NULL out");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_error(RTOW_E_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return set_error(RTOW_E_INVALID, "device out of range");
+    auto* c = new rtow_context;
+    c->device = device;
+    auto fail = [&](int rc) {
+        rtow_context_destroy(c);
+        return rc;
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    c->cus = prop.multiProcessorCount;
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    for (auto& ev : c->ev)
+        if ((e = hipEventCreate(&ev)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    if ((e = hipMalloc(&c->d_work, 64)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    *out = c;
+    return RTOW_OK;
+}
+
+int rtow_context_destroy(rtow_context* c) {
+    if (!c) return RTOW_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_scene) (void)hipFree(c->d_scene);
+    if (c->d_work) (void)hipFree(c->d_work);
+    if (c->d_partial) (void)hipFree(c->d_partial);
+    if (c->d_fb) (void)hipFree(c->d_fb);
+    for (auto& ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RTOW_OK;
+}
+
+int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_need) {
+    if (!s) return set_error(RTOW_E_INVALID, "NULL scene");
+    HostLayout L;
+    int rc = buildLayout(*s, L);
+    if (rc) return rc;
+    if (L.stack_need > 64) return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
+    if (stack_need) *stack_need = L.stack_need;
+    if (chain_need) *chain_need = L.chain_need;
+    return RTOW_OK;
+}
+
+int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
+    if (!c || !s) return set_error(RTOW_E_INVALID, "NULL argument");
+    HostLayout L;
+    int rc = buildLayout(*s, L);
+    if (rc) return rc;
+    std::vector<uint8_t> blob;
+    size_t o_bvh = pushBlob(blob, L.bvh), o_sph = pushBlob(blob, L.sph), o_msph = pushBlob(blob, L.msph);
+    size_t o_rect = pushBlob(blob, L.rect), o_inst = pushBlob(blob, L.inst), o_list = pushBlob(blob, L.list);
+    size_t o_refs = pushBlob(blob, L.refs), o_med = pushBlob(blob, L.med), o_mat = pushBlob(blob, L.mat);
+    size_t o_tex = pushBlob(blob, L.tex), o_rv = pushBlob(blob, L.ranvec), o_perm = pushBlob(blob, L.perm);
+    size_t o_img = pushBlob(blob, L.img), o_texels = pushBlob(blob, L.texels);
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->d_scene) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipFree(c->d_scene));
+        c->d_scene = nullptr;
+        c->has_scene = false;
+    }
+    HIP_TRY(hipMalloc(&c->d_scene, blob.size()));
+    HIP_TRY(hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    uint8_t* b = (uint8_t*)c->d_scene;
+    DevScene& d = c->scene;
+    d.bvh = (const DBvh*)(b + o_bvh);
+    d.sph = (const DSphere*)(b + o_sph);
+    d.msph = (const DMSphere*)(b + o_msph);
+    d.rect = (const DRect*)(b + o_rect);
+    d.inst = (const DInst*)(b + o_inst);
+    d.list = (const DList*)(b + o_list);
+    d.refs = (const uint32_t*)(b + o_refs);
+    d.med = (const DMedium*)(b + o_med);
+    d.mat = (const DMat*)(b + o_mat);
+    d.tex = (const DTex*)(b + o_tex);
+    d.ranvec = (const float*)(b + o_rv);
+    d.perm = (const uint32_t*)(b + o_perm);
+    d.img = (const DImage*)(b + o_img);
+    d.texels = (const uint8_t*)(b + o_texels);
+    d.root = L.root;
+    d.stack_need = L.stack_need;
+    d.has_media = L.has_media ? 1u : 0u;
+    c->has_scene = true;
+    return RTOW_OK;
+}
+
+int rtow_render(rtow_context* c, const rtow_camera* cam, const rtow_params* p, uint8_t* bgra_out, float* linear_out,
+                rtow_stats* stats) {
+    if (!c || !p) return set_error(RTOW_E_INVALID, "NULL argument");
+    rtow_params q = *p;
+    q.rank = 0;
+    q.world = 1;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t npx = (size_t)q.width * q.height;
+    size_t need = npx * 4 + npx * 12 + 256;
+    int rc = ensure((void**)&c->d_fb, &c->fb_bytes, need);
+    if (rc) return rc;
+    uint8_t* d_bgra = c->d_fb;
+    float* d_lin = (float*)(c->d_fb + ((npx * 4 + 255) & ~size_t(255)));
+    rc = renderCore(c, cam, &q, nullptr, nullptr, d_bgra, linear_out ? d_lin : nullptr, c->stream, stats);
+    if (rc) return rc;
+    if (bgra_out) HIP_TRY(hipMemcpy(bgra_out, d_bgra, npx * 4, hipMemcpyDeviceToHost));
+    if (linear_out) HIP_TRY(hipMemcpy(linear_out, d_lin, npx * 12, hipMemcpyDeviceToHost));
+    return RTOW_OK;
+}
+
+int rtow_render_tiles_device(rtow_context* c, const rtow_camera* cam, const rtow_params* p, void* d_bgra_slab,
+                             void* d_linear_slab, void* stream, rtow_stats* stats) {
+    if (!c) return set_error(RTOW_E_INVALID, "NULL context");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return renderCore(c, cam, p, (uint8_t*)d_bgra_slab, (float*)d_linear_slab, nullptr, nullptr, st, stats);
+}
+
+int rtow_assemble_device(rtow_context* c, uint32_t width, uint32_t height, uint32_t world, const void* d_slabs,
+                         uint32_t slab_stride_px, void* d_bgra_frame, void* stream) {
+    if (!c || !d_slabs || !d_bgra_frame || width == 0 || height == 0) return set_error(RTOW_E_INVALID, "bad arguments");
+    if (world == 0) world = 1;
+    if (slab_stride_px < rtow_rank_tile_count(width, height, 0, world) * 64u)
+        return set_error(RTOW_E_INVALID, "slab stride smaller than rank 0's slab");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIP_TRY(hipSetDevice(c->device));
+    const uint32_t n = width * height;
+    hipLaunchKernelGGL(assemble_kernel, dim3((n + 255) / 256), dim3(256), 0, st, width, height, world, (width + 7) / 8,
+                       (const uint32_t*)d_slabs, slab_stride_px, (uint32_t*)d_bgra_frame);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    return RTOW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+// rtow_device_layout.h — the scene as the gfx950 kernels read it from HBM.
+//
+// rtow_scene_upload() converts the scene graph (include/rtow.h, one record per
+// reference object) into these arrays:
+//
+//   * references are tagged 32-bit words: kind in bits 28..31, index below;
+//   * every reference BvhNode becomes a 64-byte DBvh holding BOTH children's
+//     boxes as an x/y/z-plane SoA (three float4 + the two child refs), so one
+//     node visit is four 16-byte loads and two slab tests, and traversal can
+//     visit the nearer child first.  A BvhNode with left == right
+//     (bvhNode.h:38-39, n == 1) collapses into its leaf.  The box stored for a
+//     BvhNode child is that node's own box (bvhNode.h:58); a sphere/moving
+//     sphere/rectangle child gets its exact bounding box; any other child an
+//     infinite box, so a list's buggy box (hitableList.h:52-53) never culls;
+//   * Box (box.h:43-45) becomes its 6-side list; FlipNormals/Translate/RotateY
+//     are instance records applied on the way in and, for the winning hit, on
+//     the way out (hitable.h:25-154).
+#pragma once
+
+#include <stdint.h>
+
+namespace rtow_dev {
+
+enum : uint32_t {
+    DK_BVH = 0,
+    DK_SPHERE = 1,
+    DK_MSPHERE = 2,
+    DK_RECT = 3,
+    DK_LIST = 4,
+    DK_TRANSLATE = 5,
+    DK_ROTY = 6,
+    DK_FLIP = 7,
+    DK_MEDIUM = 8,
+    DK_EXIT = 9,  // traversal-stack marker: leave the innermost instance
+    DK_NONE = 15
+};
+
+constexpr uint32_t KIND_SHIFT = 28;
+constexpr uint32_t INDEX_MASK = (1u << KIND_SHIFT) - 1;
+constexpr uint32_t mkref(uint32_t kind, uint32_t idx) { return (kind << KIND_SHIFT) | idx; }
+
+struct alignas(16) DBvh {  // 64 B
+    float xs[4];  // left.min.x, left.max.x, right.min.x, right.max.x
+    float ys[4];
+    float zs[4];
+    uint32_t left, right, pad0, pad1;
+};
+
+struct alignas(16) DSphere {  // 32 B, sphere.h:15-17
+    float c[3], r;
+    uint32_t mat, pad[3];
+};
+
+struct alignas(16) DMSphere {  // 48 B, sphere.h:87-90
+    float c0[3], r;
+    float c1[3], t0;
+    float t1;
+    uint32_t mat, pad[2];
+};
+
+struct alignas(16) DRect {  // 32 B, xy_rect.h; axis: 0 XY (k on z), 1 XZ (k on y), 2 YZ (k on x)
+    float a0, a1, b0, b1;
+    float k;
+    uint32_t axis, mat, pad;
+};
+
+struct alignas(16) DInst {  // 32 B: TRANSLATE p = offset; ROTY p[0] sin, p[1] cos; FLIP -
+    uint32_t child, pad;
+    float p[6];
+};
+
+struct alignas(16) DList {  // 16 B: children at refs[first .. first+count)
+    uint32_t first, count, pad0, pad1;
+};
+
+struct alignas(16) DMedium {  // 16 B, constantMedium.h:21-23
+    uint32_t boundary, phase_mat;
+    float density;
+    uint32_t pad;
+};
+
+struct alignas(16) DMat {  // 32 B
+    uint32_t kind, tex, needs_uv, pad;
+    float param;
+    float albedo[3];
+};
+
+struct alignas(16) DTex {  // 32 B (rtow_texture)
+    uint32_t kind, a, b, c;
+    float f[4];
+};
+
+struct alignas(16) DImage {
+    uint32_t nx, ny;
+    uint64_t offset;
+};
+
+// Pointers into one device allocation + scene-wide facts the launch needs.
+struct DevScene {
+    const DBvh* bvh;
+    const DSphere* sph;
+    const DMSphere* msph;
+    const DRect* rect;
+    const DInst* inst;
+    const DList* list;
+    const uint32_t* refs;
+    const DMedium* med;
+    const DMat* mat;
+    const DTex* tex;
+    const float* ranvec;     // 256 x float4 (xyz, pad)
+    const uint32_t* perm;    // 256 x (px | py << 8 | pz << 16)
+    const DImage* img;
+    const uint8_t* texels;
+    uint32_t root;
+    uint32_t stack_need;     // deepest traversal stack a ray can need
+    uint32_t has_media;
+};
+
+}  // namespace rtow_dev

@@ -1,0 +1,263 @@
+"""Python mirror of the C-ABI (include/rtow.h) over librtow_hip.so.
+
+Host-side plumbing for tests, bench.py and __graft_entry__: build a scene the
+way scenes.h does, upload it, render on the GPU.  The rendering itself is the
+HIP path in librtow_hip.so; there is no Python or CPU fallback -- if the
+library is missing this module raises.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "librtow_hip.so")
+HEADER = os.path.join(REPO, "include", "rtow.h")
+
+# ---- constants (include/rtow.h) ---------------------------------------------
+OK, E_INVALID, E_UNSUPPORTED, E_HIP, E_NO_DEVICE, E_IO, E_NOMEM = 0, -1, -2, -3, -4, -5, -6
+SCENE_THREE_SPHERE, SCENE_RANDOM_NED, SCENE_CORNELL_NED, SCENE_CORNELL_SMOKE = 1, 2, 3, 4
+SCENES = {"three_sphere": SCENE_THREE_SPHERE, "random_ned": SCENE_RANDOM_NED, "cornell": SCENE_CORNELL_NED,
+          "cornell_smoke": SCENE_CORNELL_SMOKE}
+IMAGE_NONE, IMAGE_SYNTHETIC, IMAGE_RAW = 0, 1, 2
+IMAGES = {"none": IMAGE_NONE, "synthetic": IMAGE_SYNTHETIC, "raw": IMAGE_RAW}
+FLAG_STATS = 1
+
+
+class Scene_(ctypes.Structure):
+    _fields_ = [("root", ctypes.c_uint32), ("n_hitables", ctypes.c_uint32), ("hitables", ctypes.c_void_p),
+                ("n_refs", ctypes.c_uint32), ("refs", ctypes.c_void_p), ("n_materials", ctypes.c_uint32),
+                ("materials", ctypes.c_void_p), ("n_textures", ctypes.c_uint32), ("textures", ctypes.c_void_p),
+                ("perlin", ctypes.c_void_p), ("n_images", ctypes.c_uint32), ("images", ctypes.c_void_p),
+                ("n_texel_bytes", ctypes.c_uint64), ("texels", ctypes.c_void_p)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("origin", ctypes.c_float * 3), ("lower_left_corner", ctypes.c_float * 3),
+                ("horizontal", ctypes.c_float * 3), ("vertical", ctypes.c_float * 3), ("u", ctypes.c_float * 3),
+                ("v", ctypes.c_float * 3), ("w", ctypes.c_float * 3), ("lens_radius", ctypes.c_float),
+                ("time0", ctypes.c_float), ("time1", ctypes.c_float)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("spp", ctypes.c_uint32),
+                ("max_depth", ctypes.c_uint32), ("gi_enable", ctypes.c_uint32), ("sky_gain", ctypes.c_float),
+                ("gi_gain", ctypes.c_float), ("samples_per_chunk", ctypes.c_uint32), ("seed", ctypes.c_uint64),
+                ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("blocks_per_cu", ctypes.c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("segments", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("pixels", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_double), ("resolve_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class BuildOpts(ctypes.Structure):
+    _fields_ = [("scene_seed", ctypes.c_uint64), ("n", ctypes.c_uint32), ("image_mode", ctypes.c_uint32),
+                ("image_path", ctypes.c_char_p), ("image_nx", ctypes.c_uint32), ("image_ny", ctypes.c_uint32),
+                ("wrap_world", ctypes.c_uint32)]
+
+
+class RtowError(RuntimeError):
+    def __init__(self, code, where, detail):
+        super().__init__(f"{where} failed: {code} ({detail})")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load librtow_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it first (python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "rtow_abi_version": ([], i32),
+        "rtow_error_string": ([i32], ctypes.c_char_p),
+        "rtow_last_error": ([], ctypes.c_char_p),
+        "rtow_params_default": ([ctypes.POINTER(Params), u32, u32, u32], None),
+        "rtow_tile_count": ([u32, u32], u32),
+        "rtow_rank_tile_count": ([u32, u32, u32, u32], u32),
+        "rtow_build_opts_default": ([ctypes.POINTER(BuildOpts)], None),
+        "rtow_build_scene": ([i32, ctypes.POINTER(BuildOpts), ctypes.POINTER(vp)], i32),
+        "rtow_scene_view": ([vp], vp),
+        "rtow_scene_free": ([vp], None),
+        "rtow_scene_save": ([vp, ctypes.c_char_p], i32),
+        "rtow_scene_load": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
+        "rtow_scene_draws": ([vp], u32),
+        "rtow_scene_check": ([vp, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
+        "rtow_camera_main": ([u32, u32, ctypes.POINTER(Camera)], i32),
+        "rtow_synthetic_image": ([u32, u32, vp], None),
+        "rtow_device_count": ([ctypes.POINTER(i32)], i32),
+        "rtow_context_create": ([i32, ctypes.POINTER(vp)], i32),
+        "rtow_context_destroy": ([vp], i32),
+        "rtow_scene_upload": ([vp, vp], i32),
+        "rtow_render": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)], i32),
+        "rtow_render_tiles_device": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, vp,
+                                      ctypes.POINTER(Stats)], i32),
+        "rtow_assemble_device": ([vp, u32, u32, u32, vp, u32, vp, vp], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def header_functions():
+    """Names of the functions include/rtow.h declares."""
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rtow_[a-z0-9_]+)\s*\(", text)))
+
+
+def check(rc, where):
+    if rc != OK:
+        L = lib()
+        raise RtowError(rc, where, f"{L.rtow_error_string(rc).decode()}: {L.rtow_last_error().decode()}")
+
+
+def params(width, height, spp, seed=1, **kw):
+    p = Params()
+    lib().rtow_params_default(ctypes.byref(p), width, height, spp)
+    p.seed = seed
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def camera_main(width, height):
+    """The camera main.cpp:111-125 builds for a width x height frame."""
+    c = Camera()
+    check(lib().rtow_camera_main(width, height, ctypes.byref(c)), "rtow_camera_main")
+    return c
+
+
+def tile_count(width, height):
+    return lib().rtow_tile_count(width, height)
+
+
+def rank_tile_count(width, height, rank, world):
+    return lib().rtow_rank_tile_count(width, height, rank, world)
+
+
+def synthetic_image(nx, ny):
+    out = np.zeros((ny, nx, 3), np.uint8)
+    lib().rtow_synthetic_image(nx, ny, out.ctypes.data)
+    return out
+
+
+class Scene:
+    """A flattened world (owned by the library)."""
+
+    def __init__(self, handle):
+        self._h = ctypes.c_void_p(handle)
+
+    @classmethod
+    def build(cls, scene="random_ned", n=100, image="synthetic", scene_seed=1, wrap_world=True, image_path=None,
+              image_size=(0, 0)):
+        o = BuildOpts()
+        lib().rtow_build_opts_default(ctypes.byref(o))
+        o.scene_seed = scene_seed
+        o.n = n
+        o.image_mode = IMAGES[image]
+        o.image_path = image_path.encode() if image_path else None
+        o.image_nx, o.image_ny = image_size
+        o.wrap_world = 1 if wrap_world else 0
+        h = ctypes.c_void_p()
+        check(lib().rtow_build_scene(SCENES[scene], ctypes.byref(o), ctypes.byref(h)), "rtow_build_scene")
+        return cls(h.value)
+
+    @classmethod
+    def load(cls, path):
+        h = ctypes.c_void_p()
+        check(lib().rtow_scene_load(path.encode(), ctypes.byref(h)), "rtow_scene_load")
+        return cls(h.value)
+
+    @property
+    def view_ptr(self):
+        return lib().rtow_scene_view(self._h)
+
+    @property
+    def view(self):
+        return Scene_.from_address(self.view_ptr)
+
+    @property
+    def draws(self):
+        return lib().rtow_scene_draws(self._h)
+
+    def save(self, path):
+        check(lib().rtow_scene_save(self.view_ptr, path.encode()), "rtow_scene_save")
+
+    def check(self):
+        sn, cn = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().rtow_scene_check(self.view_ptr, ctypes.byref(sn), ctypes.byref(cn)), "rtow_scene_check")
+        return sn.value, cn.value
+
+    def __del__(self):
+        try:
+            if self._h and _lib is not None:
+                _lib.rtow_scene_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    rc = lib().rtow_device_count(ctypes.byref(n))
+    return n.value if rc == OK else 0
+
+
+class Context:
+    """One GPU: its stream, the uploaded scene and the work buffers."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(lib().rtow_context_create(device, ctypes.byref(h)), "rtow_context_create")
+        self._h = h
+
+    def upload(self, scene):
+        check(lib().rtow_scene_upload(self._h, scene.view_ptr), "rtow_scene_upload")
+
+    def render(self, cam, p, linear=True):
+        """rtow_render: returns (bgra[H,W,4] uint8, linear[H,W,3] float32 or None, Stats)."""
+        bgra = np.zeros((p.height, p.width, 4), np.uint8)
+        lin = np.zeros((p.height, p.width, 3), np.float32) if linear else None
+        st = Stats()
+        check(lib().rtow_render(self._h, ctypes.byref(cam), ctypes.byref(p), bgra.ctypes.data,
+                                lin.ctypes.data if linear else None, ctypes.byref(st)), "rtow_render")
+        return bgra, lin, st
+
+    def render_tiles_device(self, cam, p, d_bgra_slab, d_lin_slab=None, stream=None):
+        """rtow_render_tiles_device on device pointers (ints); returns Stats."""
+        st = Stats()
+        check(lib().rtow_render_tiles_device(self._h, ctypes.byref(cam), ctypes.byref(p), d_bgra_slab, d_lin_slab,
+                                             stream, ctypes.byref(st)), "rtow_render_tiles_device")
+        return st
+
+    def assemble_device(self, width, height, world, d_slabs, stride_px, d_frame, stream=None):
+        check(lib().rtow_assemble_device(self._h, width, height, world, d_slabs, stride_px, d_frame, stream),
+              "rtow_assemble_device")
+
+    def close(self):
+        if self._h:
+            lib().rtow_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

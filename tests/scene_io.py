@@ -1,0 +1,206 @@
+"""Test helpers: RTOWSCN1 scene files, the synthetic texture, the C oracle.
+
+The oracle (oracle/librtow_oracle.so) is test infrastructure: tests use it as
+the checker only (see oracle/rtow_oracle.h).
+"""
+import ctypes
+import json
+import os
+import struct
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ORACLE_SO = os.path.join(REPO, "oracle", "librtow_oracle.so")
+
+HITABLE = np.dtype([("kind", "<u4"), ("a", "<u4"), ("b", "<u4"), ("c", "<u4"), ("f", "<f4", 12)])
+MATERIAL = np.dtype([("kind", "<u4"), ("texture", "<u4"), ("param", "<f4"), ("albedo", "<f4", 3),
+                     ("pad", "<u4", 2)])
+TEXTURE = np.dtype([("kind", "<u4"), ("a", "<u4"), ("b", "<u4"), ("c", "<u4"), ("f", "<f4", 4)])
+IMAGE = np.dtype([("nx", "<u4"), ("ny", "<u4"), ("channels", "<u4"), ("pad", "<u4"), ("offset", "<u8")])
+PERLIN = np.dtype([("ranfloat", "<f4", 256), ("ranvec", "<f4", (256, 3)), ("perm_x", "<i4", 256),
+                   ("perm_y", "<i4", 256), ("perm_z", "<i4", 256)])
+assert HITABLE.itemsize == 64 and MATERIAL.itemsize == 32 and TEXTURE.itemsize == 32
+assert IMAGE.itemsize == 24 and PERLIN.itemsize == 7168
+
+
+def synthetic_image(nx, ny):
+    """The synthetic stand-in for the 2048x1024 earth texture:
+    r = 255*i/(nx-1), g = 255*j/(ny-1), b = 40 + 160*checker32(i,j) + (i*j & 31)."""
+    i = np.arange(nx, dtype=np.int64)[None, :]
+    j = np.arange(ny, dtype=np.int64)[:, None]
+    r = (i * 255) // max(nx - 1, 1) + 0 * j
+    g = (j * 255) // max(ny - 1, 1) + 0 * i
+    b = 40 + 160 * (((i >> 5) + (j >> 5)) & 1) + ((i * j) & 31)
+    return np.stack([r, g, b], axis=-1).astype(np.uint8)
+
+
+def parse_scene(blob):
+    """RTOWSCN1 bytes -> dict of numpy arrays (texels may be stripped)."""
+    assert blob[:8] == b"RTOWSCN1", "not a scene file"
+    hdr = struct.unpack("<10I", blob[8:48])
+    (ntex,) = struct.unpack("<Q", blob[48:56])
+    off = 56
+    out = {"version": hdr[0], "root": hdr[1]}
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(blob, dtype=dtype, count=count, offset=off).copy()
+        off += dtype.itemsize * count
+        return a
+
+    out["hitables"] = take(HITABLE, hdr[2])
+    out["refs"] = take(np.dtype("<u4"), hdr[3])
+    out["materials"] = take(MATERIAL, hdr[4])
+    out["textures"] = take(TEXTURE, hdr[5])
+    out["perlin"] = take(PERLIN, 1)[0] if hdr[7] else None
+    out["images"] = take(IMAGE, hdr[6])
+    out["texels"] = np.frombuffer(blob, dtype=np.uint8, count=ntex, offset=off).copy()
+    off += ntex
+    assert off == len(blob), "trailing bytes in scene file"
+    return out
+
+
+def load_scene(path):
+    with open(path, "rb") as f:
+        return parse_scene(f.read())
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def golden_case(name):
+    for c in manifest()["cases"]:
+        if c["name"] == name:
+            return c
+    raise KeyError(name)
+
+
+def golden_image(name, W, H):
+    lin = np.fromfile(os.path.join(GOLDEN, name + ".lin"), dtype=np.float32).reshape(H, W, 3)
+    bgra = np.fromfile(os.path.join(GOLDEN, name + ".bgra"), dtype=np.uint8).reshape(H, W, 4)
+    return lin, bgra
+
+
+# ---- ctypes mirror of include/rtow.h structs --------------------------------
+class RtowScene(ctypes.Structure):
+    _fields_ = [("root", ctypes.c_uint32), ("n_hitables", ctypes.c_uint32), ("hitables", ctypes.c_void_p),
+                ("n_refs", ctypes.c_uint32), ("refs", ctypes.c_void_p), ("n_materials", ctypes.c_uint32),
+                ("materials", ctypes.c_void_p), ("n_textures", ctypes.c_uint32), ("textures", ctypes.c_void_p),
+                ("perlin", ctypes.c_void_p), ("n_images", ctypes.c_uint32), ("images", ctypes.c_void_p),
+                ("n_texel_bytes", ctypes.c_uint64), ("texels", ctypes.c_void_p)]
+
+
+class RtowCamera(ctypes.Structure):
+    _fields_ = [("origin", ctypes.c_float * 3), ("lower_left_corner", ctypes.c_float * 3),
+                ("horizontal", ctypes.c_float * 3), ("vertical", ctypes.c_float * 3), ("u", ctypes.c_float * 3),
+                ("v", ctypes.c_float * 3), ("w", ctypes.c_float * 3), ("lens_radius", ctypes.c_float),
+                ("time0", ctypes.c_float), ("time1", ctypes.c_float)]
+
+
+class RtowParams(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("spp", ctypes.c_uint32),
+                ("max_depth", ctypes.c_uint32), ("gi_enable", ctypes.c_uint32), ("sky_gain", ctypes.c_float),
+                ("gi_gain", ctypes.c_float), ("samples_per_chunk", ctypes.c_uint32), ("seed", ctypes.c_uint64),
+                ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("blocks_per_cu", ctypes.c_uint32)]
+
+
+class OracleCounters(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "samples", "segments", "bvh_visits", "bvh_box_pass", "sphere_tests", "moving_sphere_tests",
+        "rect_tests", "medium_calls", "list_visits", "draws", "max_draws_per_sample")]
+
+
+def camera_from_file(path):
+    cam = RtowCamera()
+    data = open(path, "rb").read()
+    assert len(data) == ctypes.sizeof(RtowCamera)
+    ctypes.memmove(ctypes.addressof(cam), data, len(data))
+    return cam
+
+
+def default_params(W, H, spp, seed=1):
+    return RtowParams(width=W, height=H, spp=spp, max_depth=50, gi_enable=1, sky_gain=1.0, gi_gain=0.3,
+                      samples_per_chunk=0, seed=seed, rank=0, world=1, flags=0, blocks_per_cu=0)
+
+
+class SceneArrays:
+    """Keeps numpy arrays alive behind an RtowScene view."""
+
+    def __init__(self, d):
+        self.d = d
+        self.perlin = np.array([d["perlin"]], dtype=PERLIN) if d["perlin"] is not None else None
+        self.view = RtowScene(
+            root=d["root"], n_hitables=len(d["hitables"]), hitables=d["hitables"].ctypes.data,
+            n_refs=len(d["refs"]), refs=d["refs"].ctypes.data if len(d["refs"]) else None,
+            n_materials=len(d["materials"]), materials=d["materials"].ctypes.data,
+            n_textures=len(d["textures"]), textures=d["textures"].ctypes.data,
+            perlin=self.perlin.ctypes.data if self.perlin is not None else None,
+            n_images=len(d["images"]), images=d["images"].ctypes.data if len(d["images"]) else None,
+            n_texel_bytes=len(d["texels"]), texels=d["texels"].ctypes.data if len(d["texels"]) else None)
+
+
+def with_synthetic_texels(d):
+    """Re-attach the synthetic texture's texels to a stripped golden scene."""
+    if len(d["images"]) == 0 or len(d["texels"]):
+        return d
+    parts = []
+    off = 0
+    imgs = d["images"].copy()
+    for k, im in enumerate(imgs):
+        rgb = synthetic_image(int(im["nx"]), int(im["ny"])).reshape(-1)
+        imgs[k]["offset"] = off
+        parts.append(rgb)
+        off += rgb.size
+    d = dict(d)
+    d["images"] = imgs
+    d["texels"] = np.concatenate(parts)
+    return d
+
+
+_oracle = None
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        lib = ctypes.CDLL(ORACLE_SO)
+        lib.rtow_oracle_render_pixels.argtypes = [ctypes.c_void_p, ctypes.POINTER(RtowCamera),
+                                                  ctypes.POINTER(RtowParams), ctypes.c_void_p, ctypes.c_uint32,
+                                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.POINTER(OracleCounters)]
+        lib.rtow_oracle_render_pixels.restype = ctypes.c_int
+        _oracle = lib
+    return _oracle
+
+
+def oracle_render(scene_view_ptr, cam, params, pixels=None, threads=None):
+    """Render with the C oracle.  scene_view_ptr: address of an rtow_scene.
+    Returns (lin [n,3] float32, bgra [n,4] uint8, counters)."""
+    lib = oracle()
+    if pixels is None:
+        n = params.width * params.height
+        pix_ptr = None
+    else:
+        pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
+        n = pixels.size
+        pix_ptr = pixels.ctypes.data
+    lin = np.zeros((n, 3), np.float32)
+    bgra = np.zeros((n, 4), np.uint8)
+    c = OracleCounters()
+    threads = threads or min(8, os.cpu_count() or 1)
+    rc = lib.rtow_oracle_render_pixels(scene_view_ptr, ctypes.byref(cam), ctypes.byref(params), pix_ptr, n,
+                                       threads, lin.ctypes.data, bgra.ctypes.data, ctypes.byref(c))
+    if rc != 0:
+        raise RuntimeError(f"oracle render failed: {rc}")
+    return lin, bgra, c
+
+
+def rms(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)))
