@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE.json config 2 -- the book-1 random scene
+(randomScene_NED with n = 487, 488 hitables under one BvhNode) at
+1920x1080x1024spp, depth 50, on N MI355X.
+
+One step = one full frame: every rank renders its share of the frame's 8x8
+tiles (rank r takes tiles r, r+N, ...) with the HIP path in librtow_hip.so,
+then one RCCL gather (torch.distributed, backend "nccl") brings the tile
+slabs to rank 0, which assembles the BGRA frame on its GPU.  Total work is
+the fixed frame, so scaling is "strong".
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--spp S] [--no-cpu]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+      --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line (value = whole-job Mray/s; Msample/s beside it).
+roofline.achieved = algorithmic bytes per launch (bytes/ray from the
+reference's own traversal counts, measured on the oracle at this scene and
+seed, times the launch's rays) / the trace kernel's mean duration from HIP
+events on the render stream.  cpu_baseline = the C oracle (a port of the
+reference loop) on the host cores over a bounded random pixel sample.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ray-tracing-one-weekend_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# algorithmic record bytes per reference traversal event
+BYTES_BVH, BYTES_SPHERE, BYTES_MSPHERE, BYTES_RECT, BYTES_MEDIUM = 32, 20, 40, 24, 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--n", type=int, default=487)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-pixels", type=int, default=8192)
+    ap.add_argument("--cpu-spp", type=int, default=1024)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_bench.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, cam, args, threads):
+    """Oracle (kind "port": the reference's render loop restated in C, bit-exact
+    with the reference build) on a bounded random pixel sample of the same
+    frame: returns the baseline dict and bytes/ray from its traversal counts."""
+    import scene_io as sio
+
+    rng = np.random.default_rng(1234)
+    W, H = args.width, args.height
+    pix = rng.choice(W * H, size=min(args.cpu_pixels, W * H), replace=False).astype(np.uint32)
+    ocam = sio.RtowCamera.from_buffer_copy(bytes(cam))
+    p = sio.default_params(W, H, args.cpu_spp, seed=args.seed)
+    t0 = time.perf_counter()
+    _, _, c = sio.oracle_render(scene.view_ptr, ocam, p, pixels=pix, threads=threads)
+    dt = time.perf_counter() - t0
+    bytes_per_ray = (c.bvh_visits * BYTES_BVH + c.sphere_tests * BYTES_SPHERE + c.moving_sphere_tests * BYTES_MSPHERE
+                     + c.rect_tests * BYTES_RECT + c.medium_calls * BYTES_MEDIUM) / max(c.segments, 1)
+    base = {"value": round(c.segments / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "msample_per_s": round(c.samples / dt / 1e6, 4), "seconds": round(dt, 2),
+            "sample": f"{len(pix)} random pixels of the {W}x{H} frame x {args.cpu_spp} spp (same scene/seed), "
+                      f"oracle/librtow_oracle.so, {threads} threads"}
+    counts = {"segments_per_sample": c.segments / max(c.samples, 1),
+              "bvh_visits_per_ray": c.bvh_visits / max(c.segments, 1),
+              "sphere_tests_per_ray": c.sphere_tests / max(c.segments, 1),
+              "moving_sphere_tests_per_ray": c.moving_sphere_tests / max(c.segments, 1)}
+    return base, bytes_per_ray, counts
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import rtow
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+
+    W, H, spp = args.width, args.height, args.spp
+    scene = rtow.Scene.build("random_ned", n=args.n, image="synthetic", scene_seed=1)
+    cam = rtow.camera_main(W, H)
+    ctx = rtow.Context(local)
+    ctx.upload(scene)
+    stride = rtow.rank_tile_count(W, H, 0, world) * 64  # rank 0 holds the most tiles
+    slab = torch.zeros(stride * 4, dtype=torch.uint8, device="cuda")
+    gathered = torch.zeros((world, stride * 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    stream = torch.cuda.current_stream().cuda_stream
+    p = rtow.params(W, H, spp, seed=args.seed, rank=rank, world=world)
+
+    def step():
+        st = ctx.render_tiles_device(cam, p, slab.data_ptr(), None, stream)
+        if distributed:
+            dist.gather(slab, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+        else:
+            gathered[0].copy_(slab)
+        if rank == 0:
+            ctx.assemble_device(W, H, world, gathered.data_ptr(), stride, frame.data_ptr(), stream)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    segs, samples, kms = 0, 0, []
+    for _ in range(args.steps):
+        st = step()
+        segs += st.segments
+        samples += st.samples
+        kms.append(st.kernel_ms)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    tot = torch.tensor([float(segs), float(samples)], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if distributed:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    segs_all, samples_all, elapsed = float(tot[0]), float(tot[1]), float(el[0])
+
+    if rank == 0:
+        threads = min(16, os.cpu_count() or 1)
+        if args.no_cpu:
+            base, bpr, counts = None, None, {}
+        else:
+            base, bpr, counts = cpu_baseline(scene, cam, args, threads)
+        mean_kms = float(np.mean(kms))
+        launch_rays = segs / max(args.steps, 1)
+        roof = None
+        if bpr is not None:
+            achieved = bpr * launch_rays / (mean_kms * 1e-3) / 1e9
+            traffic = None
+            if os.path.exists(args.pmc_json):
+                pmc = json.load(open(args.pmc_json))
+                if pmc.get("config") == [W, H, spp, args.n, world]:
+                    traffic = pmc.get("hbm_bytes_per_launch")
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "bytes_per_ray": round(bpr, 1), "kernel_ms": round(mean_kms, 2),
+                    "note": "algorithmic bytes = reference traversal record bytes (SURVEY.md 8d); scene is "
+                            "L2/LDS-resident so real HBM traffic is far lower (traffic field)"}
+        out = {
+            "metric": "Mray/s + Msample/s, random_scene 1920×1080×1024spp at 1/2/4/8 MI355X",
+            "value": round(segs_all / elapsed / 1e6, 2),
+            "unit": "Mray/s",
+            "msample_per_s": round(samples_all / elapsed / 1e6, 3),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"randomScene_NED n={args.n} ({args.n + 1} hitables under one BvhNode), "
+                                   f"{W}x{H}x{spp}spp, depth 50, synthetic 2048x1024 earth texture",
+                       "width": W, "height": H, "spp": spp, "n": args.n, "scene_seed": 1, "render_seed": args.seed,
+                       "parallelism": f"tiles8x8 interleaved over {world} rank(s) + RCCL gather to rank 0"},
+            "rays_per_sample": round(segs_all / max(samples_all, 1), 4),
+            "roofline": roof,
+            "cpu_baseline": base,
+            "oracle_counts": {k: round(v, 3) for k, v in counts.items()},
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
