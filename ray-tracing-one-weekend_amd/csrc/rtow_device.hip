@@ -30,6 +30,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -98,17 +99,6 @@ struct DevParams {
     uint32_t n_items;
 };
 
-struct Chain {
-    uint32_t r[MAXCHAIN];
-    int n;
-};
-
-struct Best {
-    float t;
-    uint32_t prim;
-    Chain ch;
-};
-
 struct Rec {
     float t, u, v;
     F3 p, n;
@@ -133,12 +123,38 @@ __device__ __forceinline__ Ray apply_inst(const DevScene& S, uint32_t ref, const
     return q;
 }
 
-__device__ __forceinline__ Ray chain_ray(const DevScene& S, const Chain& ch, int n, const Ray& w) {
+__device__ __forceinline__ Ray chain_ray(const DevScene& S, const uint32_t* ch, int n, const Ray& w) {
     Ray r = w;
 #pragma unroll
     for (int k = 0; k < MAXCHAIN; k++)
-        if (k < n) r = apply_inst(S, ch.r[k], r);
+        if (k < n) r = apply_inst(S, ch[k], r);
     return r;
+}
+
+// the way out of the instances, innermost first (hitable.h:28-36, 53-62, 137-150)
+__device__ __forceinline__ void chain_out(const DevScene& S, const uint32_t* ch, int n, F3& p, F3& nrm) {
+#pragma unroll
+    for (int k = MAXCHAIN - 1; k >= 0; k--) {
+        if (k < n) {
+            const uint32_t ref = ch[k];
+            const uint32_t ik = ref >> KIND_SHIFT;
+            const DInst& I = S.inst[ref & INDEX_MASK];
+            if (ik == DK_FLIP) {
+                nrm = neg(nrm);
+            } else if (ik == DK_TRANSLATE) {
+                p = add(p, f3(I.p[0], I.p[1], I.p[2]));
+            } else {
+                const float s = I.p[0], c = I.p[1];
+                F3 q = p, m = nrm;
+                q.x = c * p.x + s * p.z;
+                q.z = -s * p.x + c * p.z;
+                m.x = c * nrm.x + s * nrm.z;
+                m.z = -s * nrm.x + c * nrm.z;
+                p = q;
+                nrm = m;
+            }
+        }
+    }
 }
 
 __device__ __forceinline__ F3 inv_dir(F3 d) { return f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
@@ -157,52 +173,55 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
     return tn <= tf;
 }
 
-// sphere.h:20-69: returns the root the reference would record, in (tmin, tmax)
-__device__ __forceinline__ bool sphere_t(F3 c, float R, const Ray& r, float tmin, float tmax, float& t) {
-    const F3 oc = sub(r.o, c);
+// ---- spheres: Sphere::hit sphere.h:20-69 and MovingSphere::hit sphere.h:93-118
+struct Sph {
+    F3 c0;
+    float r;
+    F3 c1;
+    float t0, t1;
+    uint32_t mat, moving;
+};
+
+__device__ __forceinline__ Sph load_sph(const DSphere* p) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0];
+    const float4 b = reinterpret_cast<const float4*>(p)[1];
+    const uint4 c = reinterpret_cast<const uint4*>(p)[2];
+    Sph s;
+    s.c0 = f3(a.x, a.y, a.z);
+    s.r = a.w;
+    s.c1 = f3(b.x, b.y, b.z);
+    s.t0 = b.w;
+    s.t1 = __uint_as_float(c.x);
+    s.mat = c.y;
+    s.moving = c.z;
+    return s;
+}
+
+// sphere.h:129-131 (a static sphere: c1 == c0, so this is c0 exactly)
+template <bool UNIT_TIME>
+__device__ __forceinline__ F3 sph_center(const Sph& s, float time) {
+    const float f = UNIT_TIME ? time : (time - s.t0) / (s.t1 - s.t0);  // (time-0)/(1-0) == time exactly
+    return add(s.c0, scl(f, sub(s.c1, s.c0)));
+}
+
+// the root the reference records, strictly inside (tmin, tmax)
+template <bool UNIT_TIME>
+__device__ __forceinline__ bool sph_t(const Sph& s, const Ray& r, float tmin, float tmax, float& t) {
+    const F3 oc = sub(r.o, sph_center<UNIT_TIME>(s, r.time));
     const float a = dot(r.d, r.d);
     const float b = dot(r.d, oc);
-    const float cc = dot(oc, oc) - R * R;
-    const float disc = b * b - a * cc;
-    if (disc > 0) {
-        const float sq = sqrtf(b * b - a * cc);
-        float temp = (-b - sq) / a;
-        if (temp < tmax && temp > tmin) {
-            t = temp;
-            return true;
-        }
-        temp = (-b + sq) / a;
-        if (temp < tmax && temp > tmin) {
-            t = temp;
-            return true;
-        }
-    }
-    return false;
-}
-
-// sphere.h:129-131
-__device__ __forceinline__ F3 msphere_center(const DMSphere& m, float time) {
-    const F3 c0 = ld3(m.c0), c1 = ld3(m.c1);
-    return add(c0, scl((time - m.t0) / (m.t1 - m.t0), sub(c1, c0)));
-}
-
-// sphere.h:93-118 (note: dot(oc, d) here, dot(d, oc) in Sphere::hit -- equal)
-__device__ __forceinline__ bool msphere_t(const DMSphere& m, const Ray& r, float tmin, float tmax, float& t) {
-    const F3 oc = sub(r.o, msphere_center(m, r.time));
-    const float a = dot(r.d, r.d);
-    const float b = dot(oc, r.d);
-    const float c = dot(oc, oc) - m.r * m.r;
+    const float c = dot(oc, oc) - s.r * s.r;
     const float disc = b * b - a * c;
     if (disc > 0) {
         const float sq = sqrtf(disc);
-        float temp = (-b - sq) / a;
-        if (temp < tmax && temp > tmin) {
-            t = temp;
+        const float tn = (-b - sq) / a;
+        if (tn < tmax && tn > tmin) {
+            t = tn;
             return true;
         }
-        temp = (-b + sq) / a;
-        if (temp < tmax && temp > tmin) {
-            t = temp;
+        const float tf = (-b + sq) / a;
+        if (tf < tmax && tf > tmin) {
+            t = tf;
             return true;
         }
     }
@@ -227,23 +246,112 @@ __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, f
     return true;
 }
 
-__device__ __forceinline__ void chain_push(Chain& ch, uint32_t ref) {
-#pragma unroll
-    for (int k = 0; k < MAXCHAIN; k++)
-        if (k == ch.n) ch.r[k] = ref;
-    ch.n++;
+// ---------------------------------------------------------------------------
+// One BvhNode step (bvhNode.h:66-96 semantics): both child boxes are tested;
+// sphere children are tested right here (right child first, so that on an
+// exact tie the right one wins, as bvhNode.h:74-77 decides); of the inner
+// children that are hit the nearer is returned and the farther pushed.
+// Returns the next node to visit, or DK_NONE to pop.
+template <bool UNIT_TIME, int STACK>
+__device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, const Ray& r, const F3& inv, float tmin,
+                                             float& bt, uint32_t& best, uint32_t* stk, int& sp, uint32_t& overflow) {
+    const DBvh* n = S.bvh + idx;
+    const float4 xs = reinterpret_cast<const float4*>(n)[0];
+    const float4 ys = reinterpret_cast<const float4*>(n)[1];
+    const float4 zs = reinterpret_cast<const float4*>(n)[2];
+    const uint4 lr = reinterpret_cast<const uint4*>(n)[3];
+    float tl, tr;
+    const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, r.o, inv, tmin, bt, tl);
+    const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, r.o, inv, tmin, bt, tr);
+    const bool lleaf = (lr.x >> KIND_SHIFT) == DK_SPHERE;
+    const bool rleaf = (lr.y >> KIND_SHIFT) == DK_SPHERE;
+    if (hr && rleaf) {
+        float t;
+        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.y & INDEX_MASK)), r, tmin, bt, t)) {
+            bt = t;
+            best = lr.y;
+        }
+    }
+    if (hl && lleaf) {
+        float t;
+        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.x & INDEX_MASK)), r, tmin, bt, t)) {
+            bt = t;
+            best = lr.x;
+        }
+    }
+    const bool li = hl && !lleaf, ri = hr && !rleaf;
+    if (li && ri) {
+        const bool lfirst = tl <= tr;
+        if (sp < STACK) {
+            stk[sp * BLOCK] = lfirst ? lr.y : lr.x;
+            sp++;
+        } else {
+            overflow = 1;
+        }
+        return lfirst ? lr.x : lr.y;
+    }
+    if (li) return lr.x;
+    if (ri) return lr.y;
+    return mkref(DK_NONE, 0);
 }
 
-// ---------------------------------------------------------------------------
-// Closest hit of `root` for a world-space ray, reference semantics.
-// stk: this lane's LDS stack column (entry e at stk[e * BLOCK]).
+// Closest hit in a world of BvhNodes and spheres only (a "simple" scene),
+// ray already in the BVH's frame.  Returns the winning sphere ref or DK_NONE.
+template <bool UNIT_TIME, int STACK>
+__device__ uint32_t trace_simple(const DevScene& S, uint32_t root, const Ray& r, float tmin, float& bt, uint32_t* stk,
+                                 uint32_t& overflow) {
+    const F3 inv = inv_dir(r.d);
+    uint32_t best = mkref(DK_NONE, 0);
+    if ((root >> KIND_SHIFT) == DK_SPHERE) {
+        float t;
+        if (sph_t<UNIT_TIME>(load_sph(S.sph + (root & INDEX_MASK)), r, tmin, bt, t)) {
+            bt = t;
+            best = root;
+        }
+        return best;
+    }
+    uint32_t cur = root;
+    int sp = 0;
+    while (true) {
+        cur = bvh_step<UNIT_TIME, STACK>(S, cur & INDEX_MASK, r, inv, tmin, bt, best, stk, sp, overflow);
+        if ((cur >> KIND_SHIFT) == DK_NONE) {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * BLOCK];
+        }
+    }
+    return best;
+}
+
+struct Best {
+    float t;
+    uint32_t prim;
+    uint32_t ch[MAXCHAIN];
+    int n;
+};
+
+__device__ __forceinline__ void chain_push(uint32_t* ch, int& n, uint32_t ref) {
+#pragma unroll
+    for (int k = 0; k < MAXCHAIN; k++)
+        if (k == n) ch[k] = ref;
+    n++;
+}
+
+__device__ __forceinline__ void take_best(Best& b, uint32_t prim, const uint32_t* ch, int n) {
+    b.prim = prim;
+#pragma unroll
+    for (int k = 0; k < MAXCHAIN; k++) b.ch[k] = ch[k];
+    b.n = n;
+}
+
+// Closest hit of `root` for a world-space ray, reference semantics, any scene
+// graph: lists in order with a shrinking tmax (hitableList.h:20-38),
+// instances, rectangles, media.  stk: this lane's LDS stack column.
 template <bool MEDIA, int STACK>
 __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, float tmin, float tmax, uint32_t* stk,
                          int sp0, Rng& rng, Best& best, uint32_t& overflow) {
-    Chain ch;
-#pragma unroll
-    for (int k = 0; k < MAXCHAIN; k++) ch.r[k] = 0;
-    ch.n = 0;
+    uint32_t ch[MAXCHAIN] = {0, 0, 0, 0};
+    int cn = 0;
     Ray r = wray;
     F3 inv = inv_dir(r.d);
     float bt = tmax;
@@ -251,58 +359,34 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
     uint32_t cur = root;
     int sp = sp0;
     while (true) {
-        const uint32_t kind = cur >> KIND_SHIFT;
+        uint32_t kind = cur >> KIND_SHIFT;
         const uint32_t idx = cur & INDEX_MASK;
-        bool pop = true;
         if (kind == DK_BVH) {
-            const DBvh& n = S.bvh[idx];
-            const float4 xs = *reinterpret_cast<const float4*>(n.xs);
-            const float4 ys = *reinterpret_cast<const float4*>(n.ys);
-            const float4 zs = *reinterpret_cast<const float4*>(n.zs);
-            const uint2 lr = *reinterpret_cast<const uint2*>(&n.left);
-            float tl, tr;
-            const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, r.o, inv, tmin, bt, tl);
-            const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, r.o, inv, tmin, bt, tr);
-            if (hl && hr) {
-                const bool lfirst = tl <= tr;
-                if (sp < STACK) {
-                    stk[sp * BLOCK] = lfirst ? lr.y : lr.x;
-                    sp++;
-                } else {
-                    overflow = 1;
-                }
-                cur = lfirst ? lr.x : lr.y;
-                pop = false;
-            } else if (hl) {
-                cur = lr.x;
-                pop = false;
-            } else if (hr) {
-                cur = lr.y;
-                pop = false;
-            }
-        } else if (kind == DK_SPHERE) {
-            const float4 cr = *reinterpret_cast<const float4*>(S.sph[idx].c);
-            float t;
-            if (sphere_t(f3(cr.x, cr.y, cr.z), cr.w, r, tmin, bt, t)) {
-                bt = t;
-                best.prim = cur;
-                best.ch = ch;
+            uint32_t b = mkref(DK_NONE, 0);
+            const uint32_t nxt = S.unit_time
+                                     ? bvh_step<true, STACK>(S, idx, r, inv, tmin, bt, b, stk, sp, overflow)
+                                     : bvh_step<false, STACK>(S, idx, r, inv, tmin, bt, b, stk, sp, overflow);
+            if ((b >> KIND_SHIFT) != DK_NONE) {
+                take_best(best, b, ch, cn);
                 found = true;
             }
-        } else if (kind == DK_MSPHERE) {
+            if ((nxt >> KIND_SHIFT) != DK_NONE) {
+                cur = nxt;
+                continue;
+            }
+        } else if (kind == DK_SPHERE) {
             float t;
-            if (msphere_t(S.msph[idx], r, tmin, bt, t)) {
+            const Sph s = load_sph(S.sph + idx);
+            if (S.unit_time ? sph_t<true>(s, r, tmin, bt, t) : sph_t<false>(s, r, tmin, bt, t)) {
                 bt = t;
-                best.prim = cur;
-                best.ch = ch;
+                take_best(best, cur, ch, cn);
                 found = true;
             }
         } else if (kind == DK_RECT) {
             float t;
             if (rect_t(S.rect[idx], r, tmin, bt, t)) {
                 bt = t;
-                best.prim = cur;
-                best.ch = ch;
+                take_best(best, cur, ch, cn);
                 found = true;
             }
         } else if (kind == DK_LIST) {
@@ -317,61 +401,55 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
                     }
                 }
                 cur = S.refs[L.first];
-                pop = false;
+                continue;
             }
         } else if (kind == DK_TRANSLATE || kind == DK_ROTY || kind == DK_FLIP) {
-            if (sp < STACK && ch.n < MAXCHAIN) {
+            if (sp < STACK && cn < MAXCHAIN) {
                 stk[sp * BLOCK] = mkref(DK_EXIT, 0);
                 sp++;
-                chain_push(ch, cur);
+                chain_push(ch, cn, cur);
                 r = apply_inst(S, cur, r);
                 inv = inv_dir(r.d);
                 cur = S.inst[idx].child;
-                pop = false;
-            } else {
-                overflow = 1;
+                continue;
             }
+            overflow = 1;
         } else if (kind == DK_EXIT) {
-            ch.n--;
-            r = chain_ray(S, ch, ch.n, wray);
+            cn--;
+            r = chain_ray(S, ch, cn, wray);
             inv = inv_dir(r.d);
         } else if (kind == DK_MEDIUM) {
-          if constexpr (MEDIA) {
-            // constantMedium.h:26-74, called with the list's current closest
-            // hit as tmax (hitableList.h:30)
-            const DMedium M = S.med[idx];
-            (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
-            Best b1, b2;
-            uint32_t dummy = 0;
-            if (traverse<false, STACK>(S, M.boundary, r, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow)) {
-                const float t1 = b1.t;
-                if (traverse<false, STACK>(S, M.boundary, r, (float)((double)t1 + 0.0001), FLT_MAX, stk, sp, rng, b2,
-                                           overflow)) {
-                    float ta = t1, tb = b2.t;
-                    if (ta < tmin) ta = tmin;
-                    if (tb > bt) tb = bt;
-                    if (!(ta >= tb)) {
-                        if (ta < 0) ta = 0;
-                        const float dl = len(r.d);
-                        const float inside = (tb - ta) * dl;
-                        const float dist = (float)(-(1 / M.density) * log(rng.next()));
-                        if (dist < inside) {
-                            bt = ta + dist / dl;
-                            best.prim = cur;
-                            best.ch = ch;
-                            found = true;
+            if constexpr (MEDIA) {
+                // constantMedium.h:26-74, called with the list's current closest
+                // hit as tmax (hitableList.h:30)
+                const DMedium M = S.med[idx];
+                (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
+                Best b1, b2;
+                if (traverse<false, STACK>(S, M.boundary, r, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow)) {
+                    const float t1 = b1.t;
+                    if (traverse<false, STACK>(S, M.boundary, r, (float)((double)t1 + 0.0001), FLT_MAX, stk, sp, rng,
+                                               b2, overflow)) {
+                        float ta = t1, tb = b2.t;
+                        if (ta < tmin) ta = tmin;
+                        if (tb > bt) tb = bt;
+                        if (!(ta >= tb)) {
+                            if (ta < 0) ta = 0;
+                            const float dl = len(r.d);
+                            const float inside = (tb - ta) * dl;
+                            const float dist = (float)(-(1 / M.density) * log(rng.next()));
+                            if (dist < inside) {
+                                bt = ta + dist / dl;
+                                take_best(best, cur, ch, cn);
+                                found = true;
+                            }
                         }
                     }
                 }
             }
-            (void)dummy;
-          }
         }
-        if (pop) {
-            if (sp == sp0) break;
-            --sp;
-            cur = stk[sp * BLOCK];
-        }
+        if (sp == sp0) break;
+        --sp;
+        cur = stk[sp * BLOCK];
     }
     best.t = bt;
     return found;
@@ -385,77 +463,59 @@ __device__ __forceinline__ void sphere_uv(F3 p, float& u, float& v) {
     v = (float)((theta + M_PI / 2) / M_PI);
 }
 
-// Build the HitRecord of the winning primitive: local ray through the chain,
-// the primitive's record, then the instances' way out, innermost first.
-__device__ void finalize(const DevScene& S, const Best& b, const Ray& wray, Rec& rec) {
-    const Ray r = chain_ray(S, b.ch, b.ch.n, wray);
-    const uint32_t kind = b.prim >> KIND_SHIFT;
-    const uint32_t idx = b.prim & INDEX_MASK;
-    rec.t = b.t;
+// The HitRecord of the winning primitive: local ray through the chain, the
+// primitive's record, then the instances' way out.
+__device__ void finalize(const DevScene& S, uint32_t prim, float t, const uint32_t* ch, int cn, const Ray& wray,
+                         Rec& rec) {
+    const Ray r = chain_ray(S, ch, cn, wray);
+    const uint32_t kind = prim >> KIND_SHIFT;
+    const uint32_t idx = prim & INDEX_MASK;
+    rec.t = t;
     rec.u = 0.0f;
     rec.v = 0.0f;
     if (kind == DK_SPHERE) {
-        const DSphere& s = S.sph[idx];
-        const F3 c = ld3(s.c);
-        rec.p = at(r, b.t);
-        rec.n = divs(sub(rec.p, c), s.r);
+        const Sph s = load_sph(S.sph + idx);
+        rec.p = at(r, t);
+        rec.n = divs(sub(rec.p, S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time)), s.r);
         rec.mat = s.mat;
-        if (S.mat[s.mat].needs_uv) sphere_uv(rec.n, rec.u, rec.v);
-    } else if (kind == DK_MSPHERE) {
-        const DMSphere& m = S.msph[idx];
-        rec.p = at(r, b.t);
-        rec.n = divs(sub(rec.p, msphere_center(m, r.time)), m.r);
-        rec.mat = m.mat;
+        if (!s.moving && S.mat[s.mat].needs_uv) sphere_uv(rec.n, rec.u, rec.v);
     } else if (kind == DK_RECT) {
         const DRect& q = S.rect[idx];
         uint32_t i, j, k;
         rect_axes(q.axis, i, j, k);
-        const float x = comp(r.o, i) + b.t * comp(r.d, i);
-        const float y = comp(r.o, j) + b.t * comp(r.d, j);
+        const float x = comp(r.o, i) + t * comp(r.d, i);
+        const float y = comp(r.o, j) + t * comp(r.d, j);
         rec.u = (x - q.a0) / (q.a1 - q.a0);
         rec.v = (y - q.b0) / (q.b1 - q.b0);
-        rec.p = at(r, b.t);
+        rec.p = at(r, t);
         rec.n = f3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
         rec.mat = q.mat;
     } else {  // DK_MEDIUM
         const DMedium& m = S.med[idx];
-        rec.p = at(r, b.t);
+        rec.p = at(r, t);
         rec.n = f3(1, 0, 0);
         rec.mat = m.phase_mat;
     }
-#pragma unroll
-    for (int k = MAXCHAIN - 1; k >= 0; k--) {
-        if (k < b.ch.n) {
-            const uint32_t ref = b.ch.r[k];
-            const uint32_t ik = ref >> KIND_SHIFT;
-            const DInst& I = S.inst[ref & INDEX_MASK];
-            if (ik == DK_FLIP) {
-                rec.n = neg(rec.n);
-            } else if (ik == DK_TRANSLATE) {
-                rec.p = add(rec.p, f3(I.p[0], I.p[1], I.p[2]));
-            } else {
-                const float s = I.p[0], c = I.p[1];
-                F3 p = rec.p, n = rec.n;
-                p.x = c * rec.p.x + s * rec.p.z;
-                p.z = -s * rec.p.x + c * rec.p.z;
-                n.x = c * rec.n.x + s * rec.n.z;
-                n.z = -s * rec.n.x + c * rec.n.z;
-                rec.p = p;
-                rec.n = n;
-            }
-        }
-    }
+    chain_out(S, ch, cn, rec.p, rec.n);
 }
 
 // ---------------------------------------------------------------------------
-// textures (texture.h, noise.h, mathUtilities.h:41-60)
-__device__ float perlin_noise(const DevScene& S, F3 p) {
+// textures (texture.h, noise.h, mathUtilities.h:41-60); Perlin tables in LDS
+struct Tables {
+    const float4* ranvec;
+    const uint32_t* perm;
+};
+
+__device__ float perlin_noise(const Tables& T, F3 p) {
     const float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
     const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
     const int i = (int)fx, j = (int)fy, k = (int)fz;
     const float uu = u * u * (3 - 2 * u);
     const float vv = v * v * (3 - 2 * v);
     const float ww = w * w * (3 - 2 * w);
+    const uint32_t px0 = T.perm[i & 255] & 255u, px1 = T.perm[(i + 1) & 255] & 255u;
+    const uint32_t py0 = (T.perm[j & 255] >> 8) & 255u, py1 = (T.perm[(j + 1) & 255] >> 8) & 255u;
+    const uint32_t pz0 = T.perm[k & 255] >> 16, pz1 = T.perm[(k + 1) & 255] >> 16;
     float accum = 0;
 #pragma unroll
     for (int di = 0; di < 2; di++)
@@ -463,9 +523,8 @@ __device__ float perlin_noise(const DevScene& S, F3 p) {
         for (int dj = 0; dj < 2; dj++)
 #pragma unroll
             for (int dk = 0; dk < 2; dk++) {
-                const uint32_t q = (S.perm[(i + di) & 255] & 255u) ^ ((S.perm[(j + dj) & 255] >> 8) & 255u) ^
-                                   ((S.perm[(k + dk) & 255] >> 16) & 255u);
-                const float4 c = *reinterpret_cast<const float4*>(S.ranvec + 4 * q);
+                const uint32_t q = (di ? px1 : px0) ^ (dj ? py1 : py0) ^ (dk ? pz1 : pz0);
+                const float4 c = T.ranvec[q];
                 const F3 wt = f3(u - di, v - dj, w - dk);
                 const float fi = di ? uu : (1 - uu);
                 const float fj = dj ? vv : (1 - vv);
@@ -475,19 +534,19 @@ __device__ float perlin_noise(const DevScene& S, F3 p) {
     return accum;
 }
 
-__device__ float turbulence(const DevScene& S, F3 p) {  // noise.h:38-49
+__device__ float turbulence(const Tables& T, F3 p) {  // noise.h:38-49
     float accum = 0;
     F3 tp = p;
     float weight = 1.0f;
     for (int i = 0; i < 7; i++) {
-        accum += weight * perlin_noise(S, tp);
+        accum += weight * perlin_noise(T, tp);
         weight *= 0.5f;
         tp = scl(2.0f, tp);
     }
     return fabsf(accum);
 }
 
-__device__ F3 tex_value(const DevScene& S, uint32_t ti, float u, float v, F3 p) {
+__device__ F3 tex_value(const DevScene& S, const Tables& T, uint32_t ti, float u, float v, F3 p) {
     for (int guard = 0; guard < 32; guard++) {
         const DTex t = S.tex[ti];
         if (t.kind == RTOW_TEX_CONSTANT) return f3(t.f[0], t.f[1], t.f[2]);
@@ -497,7 +556,7 @@ __device__ F3 tex_value(const DevScene& S, uint32_t ti, float u, float v, F3 p) 
             continue;
         }
         if (t.kind == RTOW_TEX_NOISE) {  // texture.h:44-48
-            const float s = 1 + sinf(t.f[0] * p.z + 10 * turbulence(S, p));
+            const float s = 1 + sinf(t.f[0] * p.z + 10 * turbulence(T, p));
             return scl(s, f3(0.5f, 0.5f, 0.5f));
         }
         if (t.kind == RTOW_TEX_IMAGE) {  // texture.h:65-79
@@ -544,21 +603,27 @@ __device__ __forceinline__ bool refract(F3 d, F3 n, float ni, F3& out) {  // mat
     return false;
 }
 
-__device__ __forceinline__ float schlick(float cosine, float ri) {  // material.h:28-32
+// material.h:28-32.  pow(x, 5) in double: x*x is exact (a float squared fits
+// 48 bits), two more products round at 2^-53 each, and the result is then
+// rounded to float -- it differs from libm's pow only when the double value
+// lies within ~2^-52 of a float rounding boundary (odds ~2^-28 per call).
+__device__ __forceinline__ float schlick(float cosine, float ri) {
     float r0 = (1 - ri) / (1 + ri);
     r0 = r0 * r0;
-    return (float)(r0 + (1 - r0) * pow((double)(1 - cosine), 5.0));
+    const double x = (double)(1 - cosine);
+    const double x2 = x * x;
+    return (float)(r0 + (1 - r0) * (x2 * x2 * x));
 }
 
-__device__ bool scatter(const DevScene& S, const DMat& m, const Ray& in, const Rec& rec, Rng& g, F3& atten,
-                        Ray& out) {
+__device__ bool scatter(const DevScene& S, const Tables& T, const DMat& m, const Ray& in, const Rec& rec, Rng& g,
+                        F3& atten, Ray& out) {
     switch (m.kind) {
     case RTOW_MAT_LAMBERTIAN: {  // material.h:47-53
         const F3 target = add(add(rec.p, rec.n), random_in_unit_sphere(g));
         out.o = rec.p;
         out.d = sub(target, rec.p);
         out.time = in.time;
-        atten = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        atten = tex_value(S, T, m.tex, rec.u, rec.v, rec.p);
         return true;
     }
     case RTOW_MAT_METAL: {  // material.h:62-67
@@ -575,8 +640,7 @@ __device__ bool scatter(const DevScene& S, const DMat& m, const Ray& in, const R
         F3 outward, refracted = f3(0, 0, 0);
         float ni, cosine, prob;
         atten = f3(1.0f, 1.0f, 1.0f);
-        const float dn = dot(in.d, rec.n);
-        if (dn > 0) {
+        if (dot(in.d, rec.n) > 0) {
             outward = neg(rec.n);
             ni = ri;
             cosine = ri * dot(in.d, rec.n) / len(in.d);
@@ -598,7 +662,7 @@ __device__ bool scatter(const DevScene& S, const DMat& m, const Ray& in, const R
         out.o = rec.p;
         out.d = random_in_unit_sphere(g);
         out.time = 0.0f;
-        atten = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        atten = tex_value(S, T, m.tex, rec.u, rec.v, rec.p);
         return true;
     }
     default:  // DiffuseLight never scatters (material.h:126-128)
@@ -617,15 +681,25 @@ __device__ __forceinline__ bool decode_pixel(const DevParams& P, uint32_t lp, ui
     return x < P.width && yimg < P.height;
 }
 
-template <bool MEDIA, int STACK>
-__global__ __launch_bounds__(BLOCK) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
+// MODE: 0 simple scene + unit sphere times, 1 simple scene, 2 general scene,
+// 3 general scene with media
+template <int MODE, int STACK, int WAVES>
+__global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
                                                        float4* partial, unsigned long long* counters) {
+    constexpr bool SIMPLE = MODE <= 1;
     __shared__ uint32_t s_stack[STACK * BLOCK];
+    __shared__ float4 s_ranvec[256];
+    __shared__ uint32_t s_perm[256];
+    for (uint32_t i = threadIdx.x; i < 256; i += BLOCK) {
+        s_ranvec[i] = reinterpret_cast<const float4*>(S.ranvec)[i];
+        s_perm[i] = S.perm[i];
+    }
+    __syncthreads();
+    const Tables T{s_ranvec, s_perm};
     uint32_t* stk = s_stack + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
 
-    uint32_t item = 0, s = 0, s_end = 0, pixkey = 0, depth = 0, nseg = 0, overflow = 0;
-    uint32_t col = 0, row = 0;
+    uint32_t item = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0, overflow = 0;
     bool need_item = true, need_sample = false;
     F3 acc = f3(0, 0, 0), thr = f3(1, 1, 1);
     Ray ray;
@@ -653,7 +727,6 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DevScene S, DevCam C, DevP
                 if (!decode_pixel(P, lp, x, yimg)) continue;  // padding pixel of a partial tile
                 col = x;
                 row = P.height - 1u - yimg;  // reference row numbering (main.cpp:932)
-                pixkey = row * P.width + col;
                 s = chunk * P.spc;
                 s_end = min(s + P.spc, P.spp);
                 acc = f3(0, 0, 0);
@@ -663,7 +736,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DevScene S, DevCam C, DevP
         }
         if (need_sample) {
             // main.cpp:943-946 + camera.h:123-135 (CAMERA_DOF_EN 0)
-            rng.key = rtow_sample_key(P.seed, pixkey, s);
+            rng.key = rtow_sample_key(P.seed, row * P.width + col, s);
             rng.ctr = 0;
             const float u = (float)((double)col + rng.next()) / (float)P.width;
             const float v = (float)((double)row + rng.next()) / (float)P.height;
@@ -680,19 +753,28 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DevScene S, DevCam C, DevP
 
         // ---- one segment = one color() call (color.h:12-59) ----
         nseg++;
-        Best best;
-        best.prim = 0;
-        best.ch.n = 0;
-        const bool hit = traverse<MEDIA, STACK>(S, S.root, ray, 0.001f, FLT_MAX, stk, 0, rng, best, overflow);
+        bool hit;
+        Rec rec;
+        if constexpr (SIMPLE) {
+            const Ray lray = chain_ray(S, S.root_chain, (int)S.root_chain_n, ray);
+            float bt = FLT_MAX;
+            const uint32_t prim = trace_simple<MODE == 0, STACK>(S, S.bvh_root, lray, 0.001f, bt, stk, overflow);
+            hit = (prim >> KIND_SHIFT) != DK_NONE;
+            if (hit) finalize(S, prim, bt, S.root_chain, (int)S.root_chain_n, ray, rec);
+        } else {
+            Best best;
+            best.prim = 0;
+            best.n = 0;
+            hit = traverse<MODE == 3, STACK>(S, S.root, ray, 0.001f, FLT_MAX, stk, 0, rng, best, overflow);
+            if (hit) finalize(S, best.prim, best.t, best.ch, best.n, ray, rec);
+        }
         bool done = true;
         F3 contrib = f3(0, 0, 0);
         if (hit) {
-            Rec rec;
-            finalize(S, best, ray, rec);
             const DMat m = S.mat[rec.mat];
             Ray sc;
             F3 att;
-            if (depth < P.max_depth && scatter(S, m, ray, rec, rng, att, sc)) {
+            if (depth < P.max_depth && scatter(S, T, m, ray, rec, rng, att, sc)) {
                 // emitted() is (0,0,0) for every material that scatters
                 // (material.h:38-40; DiffuseLight never scatters), so the
                 // recursion's `emitted + attenuation * color(...)` is a product
@@ -701,7 +783,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DevScene S, DevCam C, DevP
                 depth++;
                 done = false;
             } else if (m.kind == RTOW_MAT_DIFFUSE_LIGHT) {
-                contrib = mulv(thr, tex_value(S, m.tex, rec.u, rec.v, rec.p));
+                contrib = mulv(thr, tex_value(S, T, m.tex, rec.u, rec.v, rec.p));
             }
         } else if (P.gi_enable) {
             if (depth < 1) {  // color.h:35-50
@@ -812,7 +894,6 @@ namespace {
 struct HostLayout {
     std::vector<DBvh> bvh;
     std::vector<DSphere> sph;
-    std::vector<DMSphere> msph;
     std::vector<DRect> rect;
     std::vector<DInst> inst;
     std::vector<DList> list;
@@ -828,7 +909,21 @@ struct HostLayout {
     uint32_t stack_need = 0;
     uint32_t chain_need = 0;
     bool has_media = false;
+    bool simple = false;
+    bool unit_time = true;
+    uint32_t root_chain_n = 0;
+    uint32_t root_chain[4] = {0, 0, 0, 0};
+    uint32_t bvh_root = 0;
 };
+
+// true when everything below `ref` is BvhNodes and spheres
+bool onlyBvhSpheres(const HostLayout& L, uint32_t ref, int depth = 0) {
+    const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+    if (depth > 200) return false;
+    if (kind == DK_SPHERE) return true;
+    if (kind != DK_BVH) return false;
+    return onlyBvhSpheres(L, L.bvh[idx].left, depth + 1) && onlyBvhSpheres(L, L.bvh[idx].right, depth + 1);
+}
 
 struct Converter {
     const rtow_scene& s;
@@ -882,27 +977,22 @@ struct Converter {
         const rtow_hitable& h = s.hitables[hi];
         uint32_t ref = mkref(DK_NONE, 0);
         switch (h.kind) {
-        case RTOW_HIT_SPHERE: {
-            DSphere d{};
-            for (int a = 0; a < 3; a++) d.c[a] = h.f[a];
-            d.r = h.f[3];
-            d.mat = h.a;
-            ref = mkref(DK_SPHERE, (uint32_t)L.sph.size());
-            L.sph.push_back(d);
-            break;
-        }
+        case RTOW_HIT_SPHERE:
         case RTOW_HIT_MOVING_SPHERE: {
-            DMSphere d{};
+            // one leaf format for both classes (rtow_device_layout.h)
+            DSphere d{};
+            const bool moving = h.kind == RTOW_HIT_MOVING_SPHERE;
             for (int a = 0; a < 3; a++) {
                 d.c0[a] = h.f[a];
-                d.c1[a] = h.f[3 + a];
+                d.c1[a] = moving ? h.f[3 + a] : h.f[a];
             }
-            d.t0 = h.f[6];
-            d.t1 = h.f[7];
-            d.r = h.f[8];
+            d.t0 = moving ? h.f[6] : 0.0f;
+            d.t1 = moving ? h.f[7] : 1.0f;
+            d.r = moving ? h.f[8] : h.f[3];
             d.mat = h.a;
-            ref = mkref(DK_MSPHERE, (uint32_t)L.msph.size());
-            L.msph.push_back(d);
+            d.moving = moving ? 1u : 0u;
+            ref = mkref(DK_SPHERE, (uint32_t)L.sph.size());
+            L.sph.push_back(d);
             break;
         }
         case RTOW_HIT_RECT_XY:
@@ -1078,6 +1168,23 @@ int buildLayout(const rtow_scene& s, HostLayout& L) {
     L.chain_need = nb.second;
     if (L.chain_need > (uint32_t)MAXCHAIN)
         return set_error(RTOW_E_UNSUPPORTED, "instance nesting deeper than " + std::to_string(MAXCHAIN));
+    for (const DSphere& sp : L.sph)
+        if (sp.t0 != 0.0f || sp.t1 != 1.0f) L.unit_time = false;
+    {
+        uint32_t r = L.root;
+        uint32_t n = 0;
+        while (n < (uint32_t)MAXCHAIN) {
+            const uint32_t k = r >> KIND_SHIFT;
+            if (k != DK_TRANSLATE && k != DK_ROTY && k != DK_FLIP) break;
+            L.root_chain[n++] = r;
+            r = L.inst[r & INDEX_MASK].child;
+        }
+        if (onlyBvhSpheres(L, r)) {
+            L.simple = true;
+            L.root_chain_n = n;
+            L.bvh_root = r;
+        }
+    }
     for (uint32_t i = 0; i < s.n_materials; i++) {
         const rtow_material& m = s.materials[i];
         DMat d{};
@@ -1118,7 +1225,6 @@ int buildLayout(const rtow_scene& s, HostLayout& L) {
     // keep every array non-empty so each gets a valid device pointer
     if (L.bvh.empty()) L.bvh.push_back(DBvh{});
     if (L.sph.empty()) L.sph.push_back(DSphere{});
-    if (L.msph.empty()) L.msph.push_back(DMSphere{});
     if (L.rect.empty()) L.rect.push_back(DRect{});
     if (L.inst.empty()) L.inst.push_back(DInst{});
     if (L.list.empty()) L.list.push_back(DList{});
@@ -1134,6 +1240,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L) {
 struct rtow_context {
     int device = 0;
     int cus = 0;
+    int waves = 4;  // trace-kernel occupancy variant (RTOW_TRACE_WAVES; 4 measured best, tools/probe.py)
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     // scene
@@ -1168,28 +1275,48 @@ int ensure(void** p, size_t* have, size_t need) {
     return RTOW_OK;
 }
 
-template <bool MEDIA, int STACK>
+template <int MODE, int STACK, int WAVES>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     int occ = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MEDIA, STACK>, BLOCK, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES>, BLOCK, 0));
     if (occ < 1) occ = 1;
     uint32_t per = bpc ? bpc : (uint32_t)occ;
     uint32_t grid = (uint32_t)c->cus * per;
     uint32_t maxUseful = (P.n_items + BLOCK - 1) / BLOCK;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
-    hipLaunchKernelGGL((trace_kernel<MEDIA, STACK>), dim3(grid), dim3(BLOCK), 0, st, c->scene, cam, P,
+    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES>), dim3(grid), dim3(BLOCK), 0, st, c->scene, cam, P,
                        (uint32_t*)c->d_work, c->d_partial, (unsigned long long*)((uint8_t*)c->d_work + 8));
     HIP_TRY(hipGetLastError());
     return RTOW_OK;
 }
 
-int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+// occupancy variants (waves per SIMD the register allocator must allow):
+// c->waves picks one; 0 = the compiler's free choice
+template <int MODE, int STACK>
+int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+    if constexpr (STACK <= 32) {
+        if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
+        if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
+        if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
+    }
+    return launchTrace<MODE, STACK, 1>(c, cam, P, bpc, st);
+}
+
+template <int MODE>
+int launchStack(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const uint32_t need = c->scene.stack_need;
-    const bool media = c->scene.has_media != 0;
-    if (need <= 16) return media ? launchTrace<true, 16>(c, cam, P, bpc, st) : launchTrace<false, 16>(c, cam, P, bpc, st);
-    if (need <= 32) return media ? launchTrace<true, 32>(c, cam, P, bpc, st) : launchTrace<false, 32>(c, cam, P, bpc, st);
-    if (need <= 64) return media ? launchTrace<true, 64>(c, cam, P, bpc, st) : launchTrace<false, 64>(c, cam, P, bpc, st);
+    if (need <= 16) return launchWaves<MODE, 16>(c, cam, P, bpc, st);
+    if (need <= 32) return launchWaves<MODE, 32>(c, cam, P, bpc, st);
+    if (need <= 64) return launchWaves<MODE, 64>(c, cam, P, bpc, st);
     return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
+}
+
+int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+    const DevScene& d = c->scene;
+    if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
+    if (d.simple) return launchStack<1>(c, cam, P, bpc, st);
+    if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
+    return launchStack<3>(c, cam, P, bpc, st);
 }
 
 int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
@@ -1329,6 +1456,7 @@ int rtow_context_create(int device, rtow_context** out) {
     e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     c->cus = prop.multiProcessorCount;
+    if (const char* w = std::getenv("RTOW_TRACE_WAVES")) c->waves = std::atoi(w);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
@@ -1370,7 +1498,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     int rc = buildLayout(*s, L);
     if (rc) return rc;
     std::vector<uint8_t> blob;
-    size_t o_bvh = pushBlob(blob, L.bvh), o_sph = pushBlob(blob, L.sph), o_msph = pushBlob(blob, L.msph);
+    size_t o_bvh = pushBlob(blob, L.bvh), o_sph = pushBlob(blob, L.sph);
     size_t o_rect = pushBlob(blob, L.rect), o_inst = pushBlob(blob, L.inst), o_list = pushBlob(blob, L.list);
     size_t o_refs = pushBlob(blob, L.refs), o_med = pushBlob(blob, L.med), o_mat = pushBlob(blob, L.mat);
     size_t o_tex = pushBlob(blob, L.tex), o_rv = pushBlob(blob, L.ranvec), o_perm = pushBlob(blob, L.perm);
@@ -1388,7 +1516,6 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     DevScene& d = c->scene;
     d.bvh = (const DBvh*)(b + o_bvh);
     d.sph = (const DSphere*)(b + o_sph);
-    d.msph = (const DMSphere*)(b + o_msph);
     d.rect = (const DRect*)(b + o_rect);
     d.inst = (const DInst*)(b + o_inst);
     d.list = (const DList*)(b + o_list);
@@ -1403,6 +1530,11 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.root = L.root;
     d.stack_need = L.stack_need;
     d.has_media = L.has_media ? 1u : 0u;
+    d.simple = L.simple ? 1u : 0u;
+    d.unit_time = L.unit_time ? 1u : 0u;
+    d.root_chain_n = L.root_chain_n;
+    for (int k = 0; k < 4; k++) d.root_chain[k] = L.root_chain[k];
+    d.bvh_root = L.bvh_root;
     c->has_scene = true;
     return RTOW_OK;
 }

@@ -24,7 +24,6 @@ namespace rtow_dev {
 enum : uint32_t {
     DK_BVH = 0,
     DK_SPHERE = 1,
-    DK_MSPHERE = 2,
     DK_RECT = 3,
     DK_LIST = 4,
     DK_TRANSLATE = 5,
@@ -46,16 +45,16 @@ struct alignas(16) DBvh {  // 64 B
     uint32_t left, right, pad0, pad1;
 };
 
-struct alignas(16) DSphere {  // 32 B, sphere.h:15-17
-    float c[3], r;
-    uint32_t mat, pad[3];
-};
-
-struct alignas(16) DMSphere {  // 48 B, sphere.h:87-90
+// Sphere (sphere.h:7-18) and MovingSphere (sphere.h:76-91) share one leaf:
+// a static sphere is stored with center1 = center0, time0 = 0, time1 = 1, and
+// center(time) = c0 + ((time-0)/(1-0)) * (c0-c0) = c0 exactly, so one test
+// reproduces both classes bit for bit.  `moving` keeps MovingSphere's missing
+// u,v (sphere.h:93-118 never writes them).
+struct alignas(16) DSphere {  // 48 B
     float c0[3], r;
     float c1[3], t0;
     float t1;
-    uint32_t mat, pad[2];
+    uint32_t mat, moving, pad;
 };
 
 struct alignas(16) DRect {  // 32 B, xy_rect.h; axis: 0 XY (k on z), 1 XZ (k on y), 2 YZ (k on x)
@@ -99,7 +98,6 @@ struct alignas(16) DImage {
 struct DevScene {
     const DBvh* bvh;
     const DSphere* sph;
-    const DMSphere* msph;
     const DRect* rect;
     const DInst* inst;
     const DList* list;
@@ -114,6 +112,13 @@ struct DevScene {
     uint32_t root;
     uint32_t stack_need;     // deepest traversal stack a ray can need
     uint32_t has_media;
+    // "simple" worlds: a chain of instances at the root, then only BvhNodes
+    // and spheres (the random scene) -- traversed by the BVH-only kernel
+    uint32_t simple;
+    uint32_t unit_time;      // every sphere has time0 = 0, time1 = 1
+    uint32_t root_chain_n;
+    uint32_t root_chain[4];
+    uint32_t bvh_root;       // root below the chain
 };
 
 }  // namespace rtow_dev
