@@ -261,3 +261,30 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+# ---- tile partition (the host-side statement of decode_pixel / assemble_kernel) ----
+def rank_pixels(width, height, rank, world):
+    """Framebuffer indices (y*W + x, y from the top) of rank's slab, in slab
+    order: slot s holds tile rank + s*world, 64 pixels row-major in the tile.
+    Padding pixels of partial tiles are -1."""
+    tiles_x = (width + 7) // 8
+    n = rank_tile_count(width, height, rank, world)
+    slot = np.arange(n, dtype=np.int64)[:, None]
+    q = np.arange(64, dtype=np.int64)[None, :]
+    tile = rank + slot * world
+    x = (tile % tiles_x) * 8 + (q & 7)
+    y = (tile // tiles_x) * 8 + (q >> 3)
+    idx = np.where((x < width) & (y < height), y * width + x, -1)
+    return idx.reshape(-1)
+
+
+def assemble(slabs, width, height, world):
+    """numpy mirror of assemble_kernel: slabs [world, stride_px, C] -> frame [H, W, C]."""
+    slabs = np.asarray(slabs)
+    frame = np.zeros((height * width,) + slabs.shape[2:], slabs.dtype)
+    for r in range(world):
+        idx = rank_pixels(width, height, r, world)
+        ok = idx >= 0
+        frame[idx[ok]] = slabs[r, : idx.size][ok]
+    return frame.reshape((height, width) + slabs.shape[2:])

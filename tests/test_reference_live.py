@@ -1,0 +1,37 @@
+"""Only where /root/reference exists (this container, not the GPU box): run
+the reference harness (oracle/_ref/ref_harness, compiled from the reference's
+own headers) on the REAL earth JPEG and check the C oracle against it
+bit-for-bit -- the fixtures use a synthetic texture, this closes the gap."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import scene_io as sio
+
+REF = "/root/reference/rayTracingOneWeekend"
+HARNESS = os.path.join(sio.REPO, "oracle", "_ref", "ref_harness")
+
+pytestmark = pytest.mark.skipif(not (os.path.isdir(REF) and os.path.exists(HARNESS)),
+                                reason="reference or its harness build not present")
+
+
+def test_real_earth_texture_oracle_bit_exact(tmp_path):
+    import ctypes
+
+    W, H, spp = 40, 24, 8
+    env = dict(os.environ, RTOW_SCENE_SEED="1")
+    scn, pre = str(tmp_path / "r.scn"), str(tmp_path / "r")
+    subprocess.run([HARNESS, "dump", "random_ned", scn, "--cwd", REF], env=env, check=True, capture_output=True)
+    subprocess.run([HARNESS, "render", "random_ned", str(W), str(H), str(spp), pre, "--seed", "5", "--cwd", REF],
+                   env=env, check=True)
+    subprocess.run([HARNESS, "camera", str(W), str(H), pre + ".cam"], env=env, check=True)
+    d = sio.load_scene(scn)
+    assert len(d["texels"]) == 2048 * 1024 * 3
+    arr = sio.SceneArrays(d)
+    lin, bgra, _ = sio.oracle_render(ctypes.addressof(arr.view), sio.camera_from_file(pre + ".cam"),
+                                     sio.default_params(W, H, spp, seed=5))
+    ref = np.fromfile(pre + ".lin", np.float32).reshape(-1, 3)
+    assert np.array_equal(lin.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(bgra.reshape(-1), np.fromfile(pre + ".bgra", np.uint8))
