@@ -159,16 +159,32 @@ __device__ __forceinline__ void chain_out(const DevScene& S, const uint32_t* ch,
 
 __device__ __forceinline__ F3 inv_dir(F3 d) { return f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
 
+// Per-ray slab constants.  Each plane is (x - o) * (1/d): NOT the one-fma
+// form x*(1/d) - o/d, which cancels catastrophically when the origin is far
+// from the box compared with the box's distance (the random scene sits under
+// Translate(..., (0,0,1000)): in the BVH frame o.z ~ -1000, boxes ~1 away) and
+// then culls subtrees holding the true closest hit.  x - o is exact for
+// nearby planes (Sterbenz), so the error stays within a few ulp of t.
+struct SlabRay {
+    F3 o, inv;
+};
+__device__ __forceinline__ SlabRay slab_ray(const Ray& r) {
+    SlabRay s;
+    s.o = r.o;
+    s.inv = inv_dir(r.d);
+    return s;
+}
+
 // Conservative slab test for culling (never the reference's own AABB::hit,
 // whose divisions only decide WHICH subtrees it visits, not the result).
-__device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, float z0, float z1, const F3& o,
-                                     const F3& inv, float tmin, float tmax, float& tnear) {
-    const float tx0 = (x0 - o.x) * inv.x, tx1 = (x1 - o.x) * inv.x;
-    const float ty0 = (y0 - o.y) * inv.y, ty1 = (y1 - o.y) * inv.y;
-    const float tz0 = (z0 - o.z) * inv.z, tz1 = (z1 - o.z) * inv.z;
+__device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, float z0, float z1, const SlabRay& q,
+                                     float tmin, float tmax, float& tnear) {
+    const float tx0 = (x0 - q.o.x) * q.inv.x, tx1 = (x1 - q.o.x) * q.inv.x;
+    const float ty0 = (y0 - q.o.y) * q.inv.y, ty1 = (y1 - q.o.y) * q.inv.y;
+    const float tz0 = (z0 - q.o.z) * q.inv.z, tz1 = (z1 - q.o.z) * q.inv.z;
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
     float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tf = tf + fabsf(tf) * 4.0e-7f;  // 2*gamma(3) slack: the reference's exact test can pass where ours rounds out
+    tf = tf + fabsf(tf) * 1.0e-6f;  // > 2*gamma(3): the reference's exact test can pass where ours rounds out
     tnear = tn;
     return tn <= tf;
 }
@@ -177,7 +193,7 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
 struct Sph {
     F3 c0;
     float r;
-    F3 c1;
+    F3 dc;  // center1 - center0
     float t0, t1;
     uint32_t mat, moving;
 };
@@ -189,7 +205,7 @@ __device__ __forceinline__ Sph load_sph(const DSphere* p) {
     Sph s;
     s.c0 = f3(a.x, a.y, a.z);
     s.r = a.w;
-    s.c1 = f3(b.x, b.y, b.z);
+    s.dc = f3(b.x, b.y, b.z);
     s.t0 = b.w;
     s.t1 = __uint_as_float(c.x);
     s.mat = c.y;
@@ -197,20 +213,20 @@ __device__ __forceinline__ Sph load_sph(const DSphere* p) {
     return s;
 }
 
-// sphere.h:129-131 (a static sphere: c1 == c0, so this is c0 exactly)
+// sphere.h:129-131 (a static sphere has dc = 0, so this is c0 exactly)
 template <bool UNIT_TIME>
 __device__ __forceinline__ F3 sph_center(const Sph& s, float time) {
     const float f = UNIT_TIME ? time : (time - s.t0) / (s.t1 - s.t0);  // (time-0)/(1-0) == time exactly
-    return add(s.c0, scl(f, sub(s.c1, s.c0)));
+    return add(s.c0, scl(f, s.dc));
 }
 
 // the root the reference records, strictly inside (tmin, tmax)
-template <bool UNIT_TIME>
-__device__ __forceinline__ bool sph_t(const Sph& s, const Ray& r, float tmin, float tmax, float& t) {
-    const F3 oc = sub(r.o, sph_center<UNIT_TIME>(s, r.time));
-    const float a = dot(r.d, r.d);
+// `a` = dot(d, d) is the same for every sphere a ray meets: hoisted per ray.
+__device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, float a, float tmin, float tmax,
+                                         float& t) {
+    const F3 oc = sub(r.o, center);
     const float b = dot(r.d, oc);
-    const float c = dot(oc, oc) - s.r * s.r;
+    const float c = dot(oc, oc) - radius * radius;
     const float disc = b * b - a * c;
     if (disc > 0) {
         const float sq = sqrtf(disc);
@@ -226,6 +242,11 @@ __device__ __forceinline__ bool sph_t(const Sph& s, const Ray& r, float tmin, fl
         }
     }
     return false;
+}
+
+template <bool UNIT_TIME>
+__device__ __forceinline__ bool sph_t(const Sph& s, const Ray& r, float a, float tmin, float tmax, float& t) {
+    return sph_quad(sph_center<UNIT_TIME>(s, r.time), s.r, r, a, tmin, tmax, t);
 }
 
 // xy_rect.h:22-40, 57-75, 92-110 (closed interval: t == tmax is a hit)
@@ -246,6 +267,15 @@ __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, f
     return true;
 }
 
+// Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
+struct Prof {
+    uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
+};
+__device__ __forceinline__ bool first_active_lane() {
+    const unsigned long long m = __ballot(1);
+    return (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1);
+}
+
 // ---------------------------------------------------------------------------
 // One BvhNode step (bvhNode.h:66-96 semantics): both child boxes are tested;
 // sphere children are tested right here (right child first, so that on an
@@ -253,28 +283,29 @@ __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, f
 // children that are hit the nearer is returned and the farther pushed.
 // Returns the next node to visit, or DK_NONE to pop.
 template <bool UNIT_TIME, int STACK>
-__device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, const Ray& r, const F3& inv, float tmin,
-                                             float& bt, uint32_t& best, uint32_t* stk, int& sp, uint32_t& overflow) {
+__device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
+                                             float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
+                                             uint32_t& overflow) {
     const DBvh* n = S.bvh + idx;
     const float4 xs = reinterpret_cast<const float4*>(n)[0];
     const float4 ys = reinterpret_cast<const float4*>(n)[1];
     const float4 zs = reinterpret_cast<const float4*>(n)[2];
     const uint4 lr = reinterpret_cast<const uint4*>(n)[3];
     float tl, tr;
-    const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, r.o, inv, tmin, bt, tl);
-    const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, r.o, inv, tmin, bt, tr);
+    const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, q, tmin, bt, tl);
+    const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, q, tmin, bt, tr);
     const bool lleaf = (lr.x >> KIND_SHIFT) == DK_SPHERE;
     const bool rleaf = (lr.y >> KIND_SHIFT) == DK_SPHERE;
     if (hr && rleaf) {
         float t;
-        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.y & INDEX_MASK)), r, tmin, bt, t)) {
+        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.y & INDEX_MASK)), r, a, tmin, bt, t)) {
             bt = t;
             best = lr.y;
         }
     }
     if (hl && lleaf) {
         float t;
-        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.x & INDEX_MASK)), r, tmin, bt, t)) {
+        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.x & INDEX_MASK)), r, a, tmin, bt, t)) {
             bt = t;
             best = lr.x;
         }
@@ -295,30 +326,91 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
     return mkref(DK_NONE, 0);
 }
 
-// Closest hit in a world of BvhNodes and spheres only (a "simple" scene),
-// ray already in the BVH's frame.  Returns the winning sphere ref or DK_NONE.
-template <bool UNIT_TIME, int STACK>
+// Closest hit in a world of BvhNodes and spheres only (a "simple" scene,
+// every sphere with time0 = 0, time1 = 1), ray already in the BVH's frame.
+// One DNode step (bvhNode.h:66-96 semantics): each of the two child slots is
+// either a sphere, intersected right here (right slot first, so on an exact
+// tie the right child wins as bvhNode.h:74-77 decides), or an inner child,
+// slab-tested; the nearer inner hit is visited next, the farther pushed.
+// The stack keeps its top entry in a register: a pop hands that entry to the
+// next node fetch at once while the LDS read of the new top is in flight.
+// Returns the winning sphere ref or DK_NONE.
+template <int STACK, bool PROF>
 __device__ uint32_t trace_simple(const DevScene& S, uint32_t root, const Ray& r, float tmin, float& bt, uint32_t* stk,
-                                 uint32_t& overflow) {
-    const F3 inv = inv_dir(r.d);
+                                 uint32_t& overflow, Prof& prof) {
+    const SlabRay q = slab_ray(r);
+    const float a = dot(r.d, r.d);
+    const float time = r.time;
     uint32_t best = mkref(DK_NONE, 0);
     if ((root >> KIND_SHIFT) == DK_SPHERE) {
         float t;
-        if (sph_t<UNIT_TIME>(load_sph(S.sph + (root & INDEX_MASK)), r, tmin, bt, t)) {
+        if (sph_t<true>(load_sph(S.sph + (root & INDEX_MASK)), r, a, tmin, bt, t)) {
             bt = t;
             best = root;
         }
         return best;
     }
     uint32_t cur = root;
+    uint32_t top = mkref(DK_NONE, 0);
     int sp = 0;
     while (true) {
-        cur = bvh_step<UNIT_TIME, STACK>(S, cur & INDEX_MASK, r, inv, tmin, bt, best, stk, sp, overflow);
-        if ((cur >> KIND_SHIFT) == DK_NONE) {
-            if (sp == 0) break;
-            --sp;
-            cur = stk[sp * BLOCK];
+        if constexpr (PROF) {
+            prof.lane_steps++;
+            if (first_active_lane()) prof.wave_steps++;
         }
+        const float4* np = reinterpret_cast<const float4*>(S.node + (cur & INDEX_MASK));
+        const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
+        const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
+        float tb = 0.0f, ta = 0.0f;
+        bool hb = false, ha = false;
+        // slot b (the right child) first
+        if ((refb >> KIND_SHIFT) == DK_SPHERE) {
+            // Sphere::hit / MovingSphere::hit with center = c0 + time * (c1 - c0)
+            const F3 c = add(f3(b0.x, b0.y, b0.z), scl(time, f3(b1.x, b1.y, b1.z)));
+            float t;
+            if (sph_quad(c, b0.w, r, a, tmin, bt, t)) {
+                bt = t;
+                best = refb;
+            }
+        } else {
+            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, bt, tb) && (refb >> KIND_SHIFT) == DK_BVH;
+        }
+        if ((refa >> KIND_SHIFT) == DK_SPHERE) {
+            const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
+            float t;
+            if (sph_quad(c, a0.w, r, a, tmin, bt, t)) {
+                bt = t;
+                best = refa;
+            }
+        } else {
+            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, bt, ta) && (refa >> KIND_SHIFT) == DK_BVH;
+        }
+        // one back-edge, one exit: push / descend / pop are predicated updates
+        const uint32_t NONE = mkref(DK_NONE, 0);
+        const bool afirst = ta <= tb;
+        const bool both = ha && hb;
+        uint32_t nxt = both ? (afirst ? refa : refb) : (ha ? refa : (hb ? refb : NONE));
+        if (both) {  // push the farther child; the old top goes to LDS
+            if (top != NONE) {
+                if (sp < STACK) {
+                    stk[sp * BLOCK] = top;
+                    sp++;
+                } else {
+                    overflow = 1;  // reported as an error by the host
+                }
+            }
+            top = afirst ? refb : refa;
+        }
+        if (nxt == NONE) {  // pop
+            nxt = top;
+            top = NONE;
+            if (sp > 0) {
+                --sp;
+                top = stk[sp * BLOCK];
+            }
+        }
+        if (nxt == NONE) break;
+        cur = nxt;
     }
     return best;
 }
@@ -353,7 +445,8 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
     uint32_t ch[MAXCHAIN] = {0, 0, 0, 0};
     int cn = 0;
     Ray r = wray;
-    F3 inv = inv_dir(r.d);
+    SlabRay q = slab_ray(r);
+    float a = dot(r.d, r.d);
     float bt = tmax;
     bool found = false;
     uint32_t cur = root;
@@ -364,8 +457,8 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
         if (kind == DK_BVH) {
             uint32_t b = mkref(DK_NONE, 0);
             const uint32_t nxt = S.unit_time
-                                     ? bvh_step<true, STACK>(S, idx, r, inv, tmin, bt, b, stk, sp, overflow)
-                                     : bvh_step<false, STACK>(S, idx, r, inv, tmin, bt, b, stk, sp, overflow);
+                                     ? bvh_step<true, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow)
+                                     : bvh_step<false, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow);
             if ((b >> KIND_SHIFT) != DK_NONE) {
                 take_best(best, b, ch, cn);
                 found = true;
@@ -377,7 +470,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
         } else if (kind == DK_SPHERE) {
             float t;
             const Sph s = load_sph(S.sph + idx);
-            if (S.unit_time ? sph_t<true>(s, r, tmin, bt, t) : sph_t<false>(s, r, tmin, bt, t)) {
+            if (S.unit_time ? sph_t<true>(s, r, a, tmin, bt, t) : sph_t<false>(s, r, a, tmin, bt, t)) {
                 bt = t;
                 take_best(best, cur, ch, cn);
                 found = true;
@@ -409,7 +502,8 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
                 sp++;
                 chain_push(ch, cn, cur);
                 r = apply_inst(S, cur, r);
-                inv = inv_dir(r.d);
+                q = slab_ray(r);
+                a = dot(r.d, r.d);
                 cur = S.inst[idx].child;
                 continue;
             }
@@ -417,7 +511,8 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
         } else if (kind == DK_EXIT) {
             cn--;
             r = chain_ray(S, ch, cn, wray);
-            inv = inv_dir(r.d);
+            q = slab_ray(r);
+            a = dot(r.d, r.d);
         } else if (kind == DK_MEDIUM) {
             if constexpr (MEDIA) {
                 // constantMedium.h:26-74, called with the list's current closest
@@ -681,12 +776,13 @@ __device__ __forceinline__ bool decode_pixel(const DevParams& P, uint32_t lp, ui
     return x < P.width && yimg < P.height;
 }
 
-// MODE: 0 simple scene + unit sphere times, 1 simple scene, 2 general scene,
-// 3 general scene with media
-template <int MODE, int STACK, int WAVES>
+// MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
+// chain), 2 general scene, 3 general scene with media
+template <int MODE, int STACK, int WAVES, bool PROF = false>
 __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
                                                        float4* partial, unsigned long long* counters) {
-    constexpr bool SIMPLE = MODE <= 1;
+    Prof prof{0, 0, 0, 0, 0, 0};
+    constexpr bool SIMPLE = MODE == 0;
     __shared__ uint32_t s_stack[STACK * BLOCK];
     __shared__ float4 s_ranvec[256];
     __shared__ uint32_t s_perm[256];
@@ -753,12 +849,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(DevScene S, DevCam 
 
         // ---- one segment = one color() call (color.h:12-59) ----
         nseg++;
+        if constexpr (PROF) {
+            prof.lane_iters++;
+            if (first_active_lane()) prof.wave_iters++;
+        }
         bool hit;
         Rec rec;
         if constexpr (SIMPLE) {
             const Ray lray = chain_ray(S, S.root_chain, (int)S.root_chain_n, ray);
             float bt = FLT_MAX;
-            const uint32_t prim = trace_simple<MODE == 0, STACK>(S, S.bvh_root, lray, 0.001f, bt, stk, overflow);
+            const uint32_t prim = trace_simple<STACK, PROF>(S, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
             hit = (prim >> KIND_SHIFT) != DK_NONE;
             if (hit) finalize(S, prim, bt, S.root_chain, (int)S.root_chain_n, ray, rec);
         } else {
@@ -816,6 +916,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(DevScene S, DevCam 
     if (lane == 0) {
         atomicAdd(&counters[0], (unsigned long long)v);
         if (ov) atomicAdd(&counters[1], 1ull);
+    }
+    if constexpr (PROF) {
+        uint32_t vals[5] = {prof.lane_steps, prof.wave_steps, prof.leaf_tests, prof.lane_iters, prof.wave_iters};
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            uint32_t x = vals[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+            if (lane == 0) atomicAdd(&counters[2 + k], (unsigned long long)x);
+        }
     }
 }
 
@@ -893,6 +1003,7 @@ namespace {
 
 struct HostLayout {
     std::vector<DBvh> bvh;
+    std::vector<DNode> node;
     std::vector<DSphere> sph;
     std::vector<DRect> rect;
     std::vector<DInst> inst;
@@ -984,7 +1095,7 @@ struct Converter {
             const bool moving = h.kind == RTOW_HIT_MOVING_SPHERE;
             for (int a = 0; a < 3; a++) {
                 d.c0[a] = h.f[a];
-                d.c1[a] = moving ? h.f[3 + a] : h.f[a];
+                d.dc[a] = moving ? h.f[3 + a] - h.f[a] : 0.0f;  // (_center1 - _center0), sphere.h:130
             }
             d.t0 = moving ? h.f[6] : 0.0f;
             d.t1 = moving ? h.f[7] : 1.0f;
@@ -1179,10 +1290,31 @@ int buildLayout(const rtow_scene& s, HostLayout& L) {
             L.root_chain[n++] = r;
             r = L.inst[r & INDEX_MASK].child;
         }
-        if (onlyBvhSpheres(L, r)) {
+        if (onlyBvhSpheres(L, r) && L.unit_time) {
             L.simple = true;
             L.root_chain_n = n;
             L.bvh_root = r;
+            // DNode twin of every DBvh (same index): sphere children inline
+            L.node.resize(L.bvh.size());
+            for (size_t i = 0; i < L.bvh.size(); i++) {
+                const DBvh& b = L.bvh[i];
+                DNode& d = L.node[i];
+                const uint32_t refs2[2] = {b.left, b.right};
+                for (int k = 0; k < 2; k++) {
+                    float* f = k == 0 ? d.a : d.b;
+                    uint32_t& ref = k == 0 ? d.ref_a : d.ref_b;
+                    ref = refs2[k];
+                    if ((ref >> KIND_SHIFT) == DK_SPHERE) {
+                        const DSphere& sp = L.sph[ref & INDEX_MASK];
+                        f[0] = sp.c0[0]; f[1] = sp.c0[1]; f[2] = sp.c0[2]; f[3] = sp.r;
+                        f[4] = sp.dc[0]; f[5] = sp.dc[1]; f[6] = sp.dc[2];
+                    } else {
+                        f[0] = b.xs[2 * k]; f[1] = b.ys[2 * k]; f[2] = b.zs[2 * k];
+                        f[3] = b.xs[2 * k + 1]; f[4] = b.ys[2 * k + 1]; f[5] = b.zs[2 * k + 1];
+                        f[6] = 0.0f;
+                    }
+                }
+            }
         }
     }
     for (uint32_t i = 0; i < s.n_materials; i++) {
@@ -1224,6 +1356,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L) {
     if (s.n_texel_bytes) L.texels.assign(s.texels, s.texels + s.n_texel_bytes);
     // keep every array non-empty so each gets a valid device pointer
     if (L.bvh.empty()) L.bvh.push_back(DBvh{});
+    if (L.node.empty()) L.node.push_back(DNode{});
     if (L.sph.empty()) L.sph.push_back(DSphere{});
     if (L.rect.empty()) L.rect.push_back(DRect{});
     if (L.inst.empty()) L.inst.push_back(DInst{});
@@ -1241,6 +1374,7 @@ struct rtow_context {
     int device = 0;
     int cus = 0;
     int waves = 4;  // trace-kernel occupancy variant (RTOW_TRACE_WAVES; 4 measured best, tools/probe.py)
+    int profile = 0;  // RTOW_PROFILE=1: instrumented trace kernel, counters printed to stderr
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     // scene
@@ -1275,16 +1409,16 @@ int ensure(void** p, size_t* have, size_t need) {
     return RTOW_OK;
 }
 
-template <int MODE, int STACK, int WAVES>
+template <int MODE, int STACK, int WAVES, bool PROF = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     int occ = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES>, BLOCK, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES, PROF>, BLOCK, 0));
     if (occ < 1) occ = 1;
     uint32_t per = bpc ? bpc : (uint32_t)occ;
     uint32_t grid = (uint32_t)c->cus * per;
     uint32_t maxUseful = (P.n_items + BLOCK - 1) / BLOCK;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
-    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES>), dim3(grid), dim3(BLOCK), 0, st, c->scene, cam, P,
+    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF>), dim3(grid), dim3(BLOCK), 0, st, c->scene, cam, P,
                        (uint32_t*)c->d_work, c->d_partial, (unsigned long long*)((uint8_t*)c->d_work + 8));
     HIP_TRY(hipGetLastError());
     return RTOW_OK;
@@ -1295,6 +1429,8 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
 template <int MODE, int STACK>
 int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     if constexpr (STACK <= 32) {
+        if constexpr (MODE == 0 && STACK == 16)
+            if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
         if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
         if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
         if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
@@ -1314,7 +1450,6 @@ int launchStack(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
 int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const DevScene& d = c->scene;
     if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
-    if (d.simple) return launchStack<1>(c, cam, P, bpc, st);
     if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
     return launchStack<3>(c, cam, P, bpc, st);
 }
@@ -1395,9 +1530,16 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[2], st));
-    unsigned long long host_ctr[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(host_ctr, (uint8_t*)c->d_work + 8, 16, hipMemcpyDeviceToHost, st));
+    unsigned long long host_ctr[7] = {0, 0, 0, 0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(host_ctr, (uint8_t*)c->d_work + 8, sizeof host_ctr, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (c->profile && host_ctr[3])
+        std::fprintf(stderr,
+                     "rtow-profile: segments %llu | bvh steps lane %llu wave %llu (SIMD eff %.3f, %.2f steps/ray) | "
+                     "bounce iters lane %llu wave %llu (SIMD eff %.3f)\n",
+                     host_ctr[0], host_ctr[2], host_ctr[3], (double)host_ctr[2] / (64.0 * host_ctr[3]),
+                     (double)host_ctr[2] / (double)host_ctr[0], host_ctr[5], host_ctr[6],
+                     (double)host_ctr[5] / (64.0 * (double)std::max(1ull, host_ctr[6])));
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
     if (stats) {
         float k = 0, r = 0;
@@ -1457,6 +1599,7 @@ int rtow_context_create(int device, rtow_context** out) {
     if (e != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     c->cus = prop.multiProcessorCount;
     if (const char* w = std::getenv("RTOW_TRACE_WAVES")) c->waves = std::atoi(w);
+    if (const char* pr = std::getenv("RTOW_PROFILE")) c->profile = std::atoi(pr);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
@@ -1498,7 +1641,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     int rc = buildLayout(*s, L);
     if (rc) return rc;
     std::vector<uint8_t> blob;
-    size_t o_bvh = pushBlob(blob, L.bvh), o_sph = pushBlob(blob, L.sph);
+    size_t o_bvh = pushBlob(blob, L.bvh), o_node = pushBlob(blob, L.node), o_sph = pushBlob(blob, L.sph);
     size_t o_rect = pushBlob(blob, L.rect), o_inst = pushBlob(blob, L.inst), o_list = pushBlob(blob, L.list);
     size_t o_refs = pushBlob(blob, L.refs), o_med = pushBlob(blob, L.med), o_mat = pushBlob(blob, L.mat);
     size_t o_tex = pushBlob(blob, L.tex), o_rv = pushBlob(blob, L.ranvec), o_perm = pushBlob(blob, L.perm);
@@ -1515,6 +1658,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     uint8_t* b = (uint8_t*)c->d_scene;
     DevScene& d = c->scene;
     d.bvh = (const DBvh*)(b + o_bvh);
+    d.node = (const DNode*)(b + o_node);
     d.sph = (const DSphere*)(b + o_sph);
     d.rect = (const DRect*)(b + o_rect);
     d.inst = (const DInst*)(b + o_inst);

@@ -45,14 +45,28 @@ struct alignas(16) DBvh {  // 64 B
     uint32_t left, right, pad0, pad1;
 };
 
+// Node of the "simple scene" traversal (BvhNodes + spheres, every sphere with
+// time0 = 0, time1 = 1): 64 B, two 32-B child slots.  A slot holds either an
+// inner child (box min xyz, max xyz, 0, ref DK_BVH) or the sphere leaf itself
+// (center0 xyz, radius, center1 - center0 xyz, ref DK_SPHERE | sphere index),
+// so one node fetch carries everything a step needs.  Empty: ref DK_NONE.
+struct alignas(16) DNode {
+    float a[7];
+    uint32_t ref_a;
+    float b[7];
+    uint32_t ref_b;
+};
+
 // Sphere (sphere.h:7-18) and MovingSphere (sphere.h:76-91) share one leaf:
 // a static sphere is stored with center1 = center0, time0 = 0, time1 = 1, and
 // center(time) = c0 + ((time-0)/(1-0)) * (c0-c0) = c0 exactly, so one test
 // reproduces both classes bit for bit.  `moving` keeps MovingSphere's missing
 // u,v (sphere.h:93-118 never writes them).
+// dc = center1 - center0 is computed once on the host: the same float
+// subtraction center() performs on every call (sphere.h:130).
 struct alignas(16) DSphere {  // 48 B
     float c0[3], r;
-    float c1[3], t0;
+    float dc[3], t0;
     float t1;
     uint32_t mat, moving, pad;
 };
@@ -97,6 +111,7 @@ struct alignas(16) DImage {
 // Pointers into one device allocation + scene-wide facts the launch needs.
 struct DevScene {
     const DBvh* bvh;
+    const DNode* node;       // simple scenes only
     const DSphere* sph;
     const DRect* rect;
     const DInst* inst;

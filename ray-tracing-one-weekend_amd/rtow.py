@@ -13,7 +13,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "librtow_hip.so")
+LIB_PATH = os.environ.get("RTOW_LIB") or os.path.join(PKG_DIR, "librtow_hip.so")
 HEADER = os.path.join(REPO, "include", "rtow.h")
 
 # ---- constants (include/rtow.h) ---------------------------------------------

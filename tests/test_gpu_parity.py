@@ -41,7 +41,7 @@ def test_gpu_matches_reference_golden(name, gpu_ctx):
     glin, gbgra = sio.golden_image(name, W, H)
     rms = channel_rms(lin, glin)
     exact = float(np.mean(lin == glin))
-    print(f"{name}: rms {rms} exact {exact:.4f} segments {st.segments}")
+    print(f"PARITY {name}: rms {rms} exact {exact:.4f} segments {st.segments}")
     assert np.isfinite(lin).all()
     assert (rms <= RMS_TOL).all(), rms
     # quantised frame: a handful of pixels may sit on a quantisation boundary
@@ -139,3 +139,31 @@ def test_scene_reupload_and_bad_params(gpu_ctx):
         gpu_ctx.render(cam, rtow.params(0, 8, 1))
     with pytest.raises(rtow.RtowError):
         gpu_ctx.render_tiles_device(cam, rtow.params(16, 8, 1, rank=3, world=2), 0)
+
+
+def test_full_frame_every_pixel_against_oracle(gpu_ctx):
+    """All 2,073,600 pixels of the config-2 frame (1920x1080, n=487) at 8 spp,
+    GPU vs the C oracle.  This is the test that catches a culling bound that
+    is not conservative (a missed closest hit shows up as a handful of pixels
+    off by up to 20/spp, the emitter's radiance).
+
+    The north-star bar is per-channel RMS <= 1e-4 at the benchmark's 1024 spp.
+    A rare divergent sample (a last-bit transcendental difference flipping a
+    discrete decision) costs ~L/spp in one pixel and occurs ~p*spp times per
+    pixel, so the frame RMS scales as 1/sqrt(spp): rms(1024) = rms(8)*sqrt(8/1024)."""
+    W, H, spp = 1920, 1080, 8
+    scene = rtow.Scene.build("random_ned", n=487, image="synthetic")
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, spp, seed=21)
+    _, lin, _ = gpu_ctx.render(cam, p)
+    olin, _, _ = sio.oracle_render(scene.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                   sio.RtowParams.from_buffer_copy(bytes(p)), threads=16)
+    lin = lin.reshape(-1, 3)
+    d = np.abs(lin.astype(np.float64) - olin).max(axis=1)
+    rms = channel_rms(lin, olin)
+    print(f"FULLFRAME 1920x1080x8: rms {rms} scaled-to-1024spp {rms * np.sqrt(8 / 1024)} "
+          f"pixels>1e-3 {int((d > 1e-3).sum())} bit-identical pixels {float(np.mean(d == 0)):.4f}")
+    # measured (round 1): rms ~1-2e-5 per channel, 11 of 2,073,600 pixels > 1e-3
+    assert int((d > 1e-3).sum()) <= 1e-5 * W * H
+    assert (rms <= RMS_TOL).all()  # even unscaled at 8 spp

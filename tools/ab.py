@@ -1,0 +1,64 @@
+"""A/B two builds of librtow_hip.so in ONE process, interleaved rounds.
+
+  python tools/ab.py A.so B.so [C.so ...]   (AB_SPP, AB_ROUNDS)
+Each build is loaded through its own copy of rtow.py (RTOW_LIB), renders the
+same frames; images must be identical; the kernel times are compared."""
+import importlib.util
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+RTOW_PY = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "rtow.py")
+
+
+def load(name, lib):
+    os.environ["RTOW_LIB"] = os.path.abspath(lib)
+    spec = importlib.util.spec_from_file_location(name, RTOW_PY)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    m.lib()
+    return m
+
+
+def main():
+    import torch
+
+    torch.cuda.init()
+    libs = [a for a in sys.argv[1:] if a.endswith(".so")]
+    spp = int(os.environ.get("AB_SPP", "32"))
+    rounds = int(os.environ.get("AB_ROUNDS", "3"))
+    mods = [load(f"rtow_{i}", l) for i, l in enumerate(libs)]
+    configs = [("random_ned", 487, 1920, 1080, spp), ("cornell_smoke", 100, 800, 800, spp)]
+    for name, n, W, H, s in configs:
+        runs = []
+        for m in mods:
+            sc = m.Scene.build(name, n=n, image="synthetic")
+            ctx = m.Context(0)
+            ctx.upload(sc)
+            runs.append((m, sc, ctx, m.camera_main(W, H), m.params(W, H, s, seed=1)))
+        imgs = [r[2].render(r[3], r[4], linear=True)[1] for r in runs]
+        same = all((im == imgs[0]).all() for im in imgs)
+        if not same:
+            import numpy as np
+            for i in range(1, len(imgs)):
+                d = np.abs(imgs[i] - imgs[0]).max(axis=-1)
+                print(f"  {name}: {os.path.basename(libs[i])} vs {os.path.basename(libs[0])}: "
+                      f"{int((d > 0).sum())} pixels differ, max {d.max():.3g}, "
+                      f"rms {float(np.sqrt(np.mean((imgs[i] - imgs[0]) ** 2))):.3g}", flush=True)
+        t = [[] for _ in runs]
+        for _ in range(rounds):
+            for i, (m, sc, ctx, cam, p) in enumerate(runs):
+                _, _, st = ctx.render(cam, p, linear=False)
+                t[i].append((st.kernel_ms, st.segments))
+        line = [f"{name} {W}x{H}x{s} identical={same}"]
+        for i, l in enumerate(libs):
+            ms = sorted(k for k, _ in t[i])
+            line.append(f"{os.path.basename(l)}: min {ms[0]:.1f} med {ms[len(ms)//2]:.1f} ms "
+                        f"{t[i][0][1] / ms[0] / 1e3:.0f} Mray/s")
+        print(" | ".join(line), flush=True)
+        for r in runs:
+            r[2].close()
+
+
+if __name__ == "__main__":
+    main()

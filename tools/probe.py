@@ -11,6 +11,8 @@ torch.cuda.init()
 variants = [int(v) for v in os.environ.get("PROBE_WAVES", "0,3,4,5").split(",")]
 rounds = int(os.environ.get("PROBE_ROUNDS", "2"))
 configs = [("random_ned", 487, 1920, 1080, int(os.environ.get("PROBE_SPP", "32"))), ("cornell_smoke", 100, 800, 800, 32)]
+if os.environ.get("PROBE_ONLY"):
+    configs = [c for c in configs if c[0] == os.environ["PROBE_ONLY"]]
 ctxs = {}
 for w in variants:
     os.environ["RTOW_TRACE_WAVES"] = str(w)
