@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--n", type=int, default=487)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-pixels", type=int, default=8192)
+    ap.add_argument("--cpu-pixels", type=int, default=40000)
     ap.add_argument("--cpu-spp", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_bench.json"))

@@ -335,9 +335,9 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
 // The stack keeps its top entry in a register: a pop hands that entry to the
 // next node fetch at once while the LDS read of the new top is in flight.
 // Returns the winning sphere ref or DK_NONE.
-template <int STACK, bool PROF>
-__device__ uint32_t trace_simple(const DevScene& S, uint32_t root, const Ray& r, float tmin, float& bt, uint32_t* stk,
-                                 uint32_t& overflow, Prof& prof) {
+template <int STACK, int BS, bool PROF>
+__device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t root, const Ray& r, float tmin,
+                                 float& bt, uint32_t* stk, uint32_t& overflow, Prof& prof) {
     const SlabRay q = slab_ray(r);
     const float a = dot(r.d, r.d);
     const float time = r.time;
@@ -358,7 +358,7 @@ __device__ uint32_t trace_simple(const DevScene& S, uint32_t root, const Ray& r,
             prof.lane_steps++;
             if (first_active_lane()) prof.wave_steps++;
         }
-        const float4* np = reinterpret_cast<const float4*>(S.node + (cur & INDEX_MASK));
+        const float4* np = reinterpret_cast<const float4*>(nodes + (cur & INDEX_MASK));
         const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
         const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
         float tb = 0.0f, ta = 0.0f;
@@ -393,7 +393,7 @@ __device__ uint32_t trace_simple(const DevScene& S, uint32_t root, const Ray& r,
         if (both) {  // push the farther child; the old top goes to LDS
             if (top != NONE) {
                 if (sp < STACK) {
-                    stk[sp * BLOCK] = top;
+                    stk[sp * BS] = top;
                     sp++;
                 } else {
                     overflow = 1;  // reported as an error by the host
@@ -406,7 +406,7 @@ __device__ uint32_t trace_simple(const DevScene& S, uint32_t root, const Ray& r,
             top = NONE;
             if (sp > 0) {
                 --sp;
-                top = stk[sp * BLOCK];
+                top = stk[sp * BS];
             }
         }
         if (nxt == NONE) break;
@@ -778,17 +778,32 @@ __device__ __forceinline__ bool decode_pixel(const DevParams& P, uint32_t lp, ui
 
 // MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
 // chain), 2 general scene, 3 general scene with media
-template <int MODE, int STACK, int WAVES, bool PROF = false>
-__global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
+// All LDS is one dynamic region (16-B aligned carve, no static __shared__):
+// Perlin ranvec (4 KB) | perms (1 KB) | traversal stack STACK x BS words |
+// (LDSN) the DNode array of a simple scene.
+constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn) {
+    return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0);
+}
+
+template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false>
+__global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
                                                        float4* partial, unsigned long long* counters) {
     Prof prof{0, 0, 0, 0, 0, 0};
     constexpr bool SIMPLE = MODE == 0;
-    __shared__ uint32_t s_stack[STACK * BLOCK];
-    __shared__ float4 s_ranvec[256];
-    __shared__ uint32_t s_perm[256];
-    for (uint32_t i = threadIdx.x; i < 256; i += BLOCK) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4* s_ranvec = reinterpret_cast<float4*>(smem);
+    uint32_t* s_perm = reinterpret_cast<uint32_t*>(smem + 4096);
+    uint32_t* s_stack = reinterpret_cast<uint32_t*>(smem + 5120);
+    for (uint32_t i = threadIdx.x; i < 256; i += BS) {
         s_ranvec[i] = reinterpret_cast<const float4*>(S.ranvec)[i];
         s_perm[i] = S.perm[i];
+    }
+    const DNode* nodes = S.node;
+    if constexpr (SIMPLE && LDSN) {
+        float4* s_node = reinterpret_cast<float4*>(smem + 5120 + (size_t)STACK * BS * 4);
+        const float4* g = reinterpret_cast<const float4*>(S.node);
+        for (uint32_t i = threadIdx.x; i < S.n_node * 4u; i += BS) s_node[i] = g[i];
+        nodes = reinterpret_cast<const DNode*>(s_node);
     }
     __syncthreads();
     const Tables T{s_ranvec, s_perm};
@@ -858,7 +873,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(DevScene S, DevCam 
         if constexpr (SIMPLE) {
             const Ray lray = chain_ray(S, S.root_chain, (int)S.root_chain_n, ray);
             float bt = FLT_MAX;
-            const uint32_t prim = trace_simple<STACK, PROF>(S, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
+            const uint32_t prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
             hit = (prim >> KIND_SHIFT) != DK_NONE;
             if (hit) finalize(S, prim, bt, S.root_chain, (int)S.root_chain_n, ray, rec);
         } else {
@@ -1375,6 +1390,7 @@ struct rtow_context {
     int cus = 0;
     int waves = 4;  // trace-kernel occupancy variant (RTOW_TRACE_WAVES; 4 measured best, tools/probe.py)
     int profile = 0;  // RTOW_PROFILE=1: instrumented trace kernel, counters printed to stderr
+    int lds_nodes = 1;  // simple-scene BVH staged in LDS when it fits (RTOW_LDS_NODES=0 disables; +11%, tools/ab.py)
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     // scene
@@ -1409,16 +1425,19 @@ int ensure(void** p, size_t* have, size_t need) {
     return RTOW_OK;
 }
 
-template <int MODE, int STACK, int WAVES, bool PROF = false>
+template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+    const size_t lds = lds_bytes(STACK, BS, c->scene.n_node, LDSN);
     int occ = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES, PROF>, BLOCK, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN>, BS,
+                                                         lds));
     if (occ < 1) occ = 1;
     uint32_t per = bpc ? bpc : (uint32_t)occ;
     uint32_t grid = (uint32_t)c->cus * per;
-    uint32_t maxUseful = (P.n_items + BLOCK - 1) / BLOCK;
+    uint32_t maxUseful = (P.n_items + BS - 1) / BS;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
-    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF>), dim3(grid), dim3(BLOCK), 0, st, c->scene, cam, P,
+    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN>), dim3(grid), dim3(BS), lds, st, c->scene,
+                       cam, P,
                        (uint32_t*)c->d_work, c->d_partial, (unsigned long long*)((uint8_t*)c->d_work + 8));
     HIP_TRY(hipGetLastError());
     return RTOW_OK;
@@ -1429,8 +1448,12 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
 template <int MODE, int STACK>
 int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     if constexpr (STACK <= 32) {
-        if constexpr (MODE == 0 && STACK == 16)
+        if constexpr (MODE == 0 && STACK == 16) {
             if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
+            // BVH in LDS: 512-thread blocks, 2 per CU (<= 80 KB LDS each)
+            if (c->lds_nodes && lds_bytes(STACK, 512, c->scene.n_node, true) <= 80 * 1024)
+                return launchTrace<MODE, STACK, 4, false, 512, true>(c, cam, P, bpc, st);
+        }
         if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
         if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
         if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
@@ -1600,6 +1623,7 @@ int rtow_context_create(int device, rtow_context** out) {
     c->cus = prop.multiProcessorCount;
     if (const char* w = std::getenv("RTOW_TRACE_WAVES")) c->waves = std::atoi(w);
     if (const char* pr = std::getenv("RTOW_PROFILE")) c->profile = std::atoi(pr);
+    if (const char* ln = std::getenv("RTOW_LDS_NODES")) c->lds_nodes = std::atoi(ln);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
@@ -1679,6 +1703,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.root_chain_n = L.root_chain_n;
     for (int k = 0; k < 4; k++) d.root_chain[k] = L.root_chain[k];
     d.bvh_root = L.bvh_root;
+    d.n_node = L.simple ? (uint32_t)L.node.size() : 0u;
     c->has_scene = true;
     return RTOW_OK;
 }

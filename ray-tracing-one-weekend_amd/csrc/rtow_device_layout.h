@@ -134,6 +134,7 @@ struct DevScene {
     uint32_t root_chain_n;
     uint32_t root_chain[4];
     uint32_t bvh_root;       // root below the chain
+    uint32_t n_node;         // DNode count (simple scenes)
 };
 
 }  // namespace rtow_dev

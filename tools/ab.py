@@ -24,16 +24,27 @@ def main():
     import torch
 
     torch.cuda.init()
-    libs = [a for a in sys.argv[1:] if a.endswith(".so")]
+    # each variant: path/to/lib.so[:ENV=VAL[,ENV=VAL]] (env applied when its contexts are created)
+    specs = [a for a in sys.argv[1:] if ".so" in a]
+    libs = [a.split(":")[0] for a in specs]
+    envs = [dict(kv.split("=") for kv in a.split(":")[1].split(",")) if ":" in a else {} for a in specs]
     spp = int(os.environ.get("AB_SPP", "32"))
     rounds = int(os.environ.get("AB_ROUNDS", "3"))
     mods = [load(f"rtow_{i}", l) for i, l in enumerate(libs)]
+    names = [os.path.basename(sp) for sp in specs]
     configs = [("random_ned", 487, 1920, 1080, spp), ("cornell_smoke", 100, 800, 800, spp)]
     for name, n, W, H, s in configs:
         runs = []
-        for m in mods:
+        for m, env in zip(mods, envs):
             sc = m.Scene.build(name, n=n, image="synthetic")
+            saved = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
             ctx = m.Context(0)
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
             ctx.upload(sc)
             runs.append((m, sc, ctx, m.camera_main(W, H), m.params(W, H, s, seed=1)))
         imgs = [r[2].render(r[3], r[4], linear=True)[1] for r in runs]
@@ -42,7 +53,7 @@ def main():
             import numpy as np
             for i in range(1, len(imgs)):
                 d = np.abs(imgs[i] - imgs[0]).max(axis=-1)
-                print(f"  {name}: {os.path.basename(libs[i])} vs {os.path.basename(libs[0])}: "
+                print(f"  {name}: {names[i]} vs {names[0]}: "
                       f"{int((d > 0).sum())} pixels differ, max {d.max():.3g}, "
                       f"rms {float(np.sqrt(np.mean((imgs[i] - imgs[0]) ** 2))):.3g}", flush=True)
         t = [[] for _ in runs]
@@ -51,9 +62,9 @@ def main():
                 _, _, st = ctx.render(cam, p, linear=False)
                 t[i].append((st.kernel_ms, st.segments))
         line = [f"{name} {W}x{H}x{s} identical={same}"]
-        for i, l in enumerate(libs):
+        for i, l in enumerate(names):
             ms = sorted(k for k, _ in t[i])
-            line.append(f"{os.path.basename(l)}: min {ms[0]:.1f} med {ms[len(ms)//2]:.1f} ms "
+            line.append(f"{l}: min {ms[0]:.1f} med {ms[len(ms)//2]:.1f} ms "
                         f"{t[i][0][1] / ms[0] / 1e3:.0f} Mray/s")
         print(" | ".join(line), flush=True)
         for r in runs:
