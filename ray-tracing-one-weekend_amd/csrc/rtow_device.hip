@@ -270,6 +270,7 @@ __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, f
 // Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
 struct Prof {
     uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
+    unsigned long long cyc_trav, cyc_other;  // wave cycles (s_memtime) in traversal / everything else
 };
 __device__ __forceinline__ bool first_active_lane() {
     const unsigned long long m = __ballot(1);
@@ -788,7 +789,8 @@ constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn) {
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false>
 __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
                                                        float4* partial, unsigned long long* counters) {
-    Prof prof{0, 0, 0, 0, 0, 0};
+    Prof prof{0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t_mark = PROF ? __builtin_amdgcn_s_memtime() : 0;
     constexpr bool SIMPLE = MODE == 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* s_ranvec = reinterpret_cast<float4*>(smem);
@@ -871,10 +873,20 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         bool hit;
         Rec rec;
         if constexpr (SIMPLE) {
+            if constexpr (PROF) {
+                const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                prof.cyc_other += t_now - t_mark;
+                t_mark = t_now;
+            }
             const Ray lray = chain_ray(S, S.root_chain, (int)S.root_chain_n, ray);
             float bt = FLT_MAX;
             const uint32_t prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
             hit = (prim >> KIND_SHIFT) != DK_NONE;
+            if constexpr (PROF) {
+                const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                prof.cyc_trav += t_now - t_mark;
+                t_mark = t_now;
+            }
             if (hit) finalize(S, prim, bt, S.root_chain, (int)S.root_chain_n, ray, rec);
         } else {
             Best best;
@@ -940,6 +952,10 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
             if (lane == 0) atomicAdd(&counters[2 + k], (unsigned long long)x);
+        }
+        if (lane == 0) {  // s_memtime is per wave: lane 0's copy is the wave's
+            atomicAdd(&counters[7], prof.cyc_trav);
+            atomicAdd(&counters[8], prof.cyc_other);
         }
     }
 }
@@ -1539,7 +1555,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
     size_t need = (size_t)P.n_chunks * P.n_local_px * sizeof(float4);
     rc = ensure((void**)&c->d_partial, &c->partial_bytes, std::max<size_t>(need, 16));
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(c->d_work, 0, 64, st));
+    HIP_TRY(hipMemsetAsync(c->d_work, 0, 128, st));
     const DevCam dc = makeCam(cam);
     HIP_TRY(hipEventRecord(c->ev[0], st));
     if (P.n_items) {
@@ -1553,7 +1569,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[2], st));
-    unsigned long long host_ctr[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long host_ctr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(host_ctr, (uint8_t*)c->d_work + 8, sizeof host_ctr, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (c->profile && host_ctr[3])
@@ -1563,6 +1579,10 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
                      host_ctr[0], host_ctr[2], host_ctr[3], (double)host_ctr[2] / (64.0 * host_ctr[3]),
                      (double)host_ctr[2] / (double)host_ctr[0], host_ctr[5], host_ctr[6],
                      (double)host_ctr[5] / (64.0 * (double)std::max(1ull, host_ctr[6])));
+    if (c->profile && host_ctr[7])
+        std::fprintf(stderr, "rtow-profile: wave cycles traversal %.3g other %.3g (traversal share %.3f)\n",
+                     (double)host_ctr[7], (double)host_ctr[8],
+                     (double)host_ctr[7] / (double)(host_ctr[7] + host_ctr[8]));
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
     if (stats) {
         float k = 0, r = 0;
@@ -1628,7 +1648,7 @@ int rtow_context_create(int device, rtow_context** out) {
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
-    if ((e = hipMalloc(&c->d_work, 64)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    if ((e = hipMalloc(&c->d_work, 128)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     *out = c;
     return RTOW_OK;
 }
