@@ -244,6 +244,29 @@ __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, 
     return false;
 }
 
+// Sphere::hit over the reference's whole window (tmin, MAXFLOAT) (color.h:17
+// passes MAXFLOAT), then BvhNode::hit's merge of two records (bvhNode.h:74-77):
+// the nearer wins and an exact tie goes to the later leaf of the reference
+// tree, i.e. the larger sphere index (see rebuildSah).  `bt`/`best` is the
+// record so far.  The far root is only evaluated when the near one is <= tmin.
+__device__ __forceinline__ bool sph_closer(F3 center, float radius, const Ray& r, float a, float tmin, float bt,
+                                           uint32_t best, uint32_t ref, float& t) {
+    const F3 oc = sub(r.o, center);
+    const float b = dot(r.d, oc);
+    const float c = dot(oc, oc) - radius * radius;
+    const float disc = b * b - a * c;
+    if (disc > 0) {
+        const float sq = sqrtf(disc);
+        float root = (-b - sq) / a;
+        if (!(root < FLT_MAX && root > tmin)) root = (-b + sq) / a;
+        if (root < FLT_MAX && root > tmin && (root < bt || (root == bt && ref > best))) {
+            t = root;
+            return true;
+        }
+    }
+    return false;
+}
+
 template <bool UNIT_TIME>
 __device__ __forceinline__ bool sph_t(const Sph& s, const Ray& r, float a, float tmin, float tmax, float& t) {
     return sph_quad(sph_center<UNIT_TIME>(s, r.time), s.r, r, a, tmin, tmax, t);
@@ -329,10 +352,11 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
 
 // Closest hit in a world of BvhNodes and spheres only (a "simple" scene,
 // every sphere with time0 = 0, time1 = 1), ray already in the BVH's frame.
-// One DNode step (bvhNode.h:66-96 semantics): each of the two child slots is
-// either a sphere, intersected right here (right slot first, so on an exact
-// tie the right child wins as bvhNode.h:74-77 decides), or an inner child,
-// slab-tested; the nearer inner hit is visited next, the farther pushed.
+// The tree is the SAH rebuild (rebuildSah) or the reference's own; either way
+// one DNode step tests both child slots: a sphere slot is intersected right
+// here (sph_closer: nearer wins, exact ties by the reference's leaf order, so
+// the result does not depend on the tree or the visit order), an inner slot
+// is slab-tested; the nearer inner hit is visited next, the farther pushed.
 // The stack keeps its top entry in a register: a pop hands that entry to the
 // next node fetch at once while the LDS read of the new top is in flight.
 // Returns the winning sphere ref or DK_NONE.
@@ -369,7 +393,7 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
             // Sphere::hit / MovingSphere::hit with center = c0 + time * (c1 - c0)
             const F3 c = add(f3(b0.x, b0.y, b0.z), scl(time, f3(b1.x, b1.y, b1.z)));
             float t;
-            if (sph_quad(c, b0.w, r, a, tmin, bt, t)) {
+            if (sph_closer(c, b0.w, r, a, tmin, bt, best, refb, t)) {
                 bt = t;
                 best = refb;
             }
@@ -379,7 +403,7 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
             float t;
-            if (sph_quad(c, a0.w, r, a, tmin, bt, t)) {
+            if (sph_closer(c, a0.w, r, a, tmin, bt, best, refa, t)) {
                 bt = t;
                 best = refa;
             }
@@ -1058,6 +1082,143 @@ struct HostLayout {
     uint32_t bvh_root = 0;
 };
 
+// ---------------------------------------------------------------------------
+// Simple scenes are traversed over a surface-area-heuristic tree rebuilt from
+// the same spheres instead of the reference's own BvhNode tree (bvhNode.h:
+// 14-58 sorts on a random axis and splits at the median, which leaves the
+// R=1000 ground sphere's box on a spine of whole-scene boxes every ray walks).
+// The closest hit is a property of the set of leaves, not of the tree, once
+// ties are settled the reference's way: BvhNode::hit (bvhNode.h:66-96) keeps
+// the nearer record and hands an exact tie to the right subtree, so among the
+// leaves at the minimal t the reference returns the LAST one in the tree's
+// left-to-right order.  The converter numbers spheres in that order (it
+// converts the left subtree first), so the device breaks a tie by the larger
+// sphere index, and the result is the reference tree's whatever tree is
+// traversed.  RTOW_BVH=ref keeps the reference tree.
+struct SahPrim {
+    float mn[3], mx[3], c[3];
+    uint32_t ref;
+};
+
+float sahArea(const float* mn, const float* mx) {
+    const double dx = (double)mx[0] - mn[0], dy = (double)mx[1] - mn[1], dz = (double)mx[2] - mn[2];
+    return (float)(2.0 * (dx * dy + dy * dz + dz * dx));
+}
+
+void sahUnion(float* mn, float* mx, const float* bmn, const float* bmx) {
+    for (int a = 0; a < 3; a++) {
+        mn[a] = std::min(mn[a], bmn[a]);
+        mx[a] = std::max(mx[a], bmx[a]);
+    }
+}
+
+// Binary SAH build over P[lo, hi) (full sweep over the three centroid axes);
+// fills `out` with fused DNodes (sphere children inline) and returns the
+// node's ref.  `need` = LDS stack entries its traversal can hold: a push
+// happens only where both children are inner nodes and hit.
+uint32_t sahBuild(const HostLayout& L, std::vector<SahPrim>& P, size_t lo, size_t hi, std::vector<DNode>& out,
+                  uint32_t& need, int depth) {
+    const size_t n = hi - lo;
+    const uint32_t idx = (uint32_t)out.size();
+    out.push_back(DNode{});
+    int best_axis = 0;
+    size_t best_i = lo + n / 2;
+    double best_cost = DBL_MAX;
+    std::vector<float> right_area(n + 1);
+    for (int axis = 0; axis < 3; axis++) {
+        std::sort(P.begin() + lo, P.begin() + hi, [axis](const SahPrim& x, const SahPrim& y) {
+            return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.ref < y.ref);
+        });
+        float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = n; k-- > 1;) {
+            sahUnion(mn, mx, P[lo + k].mn, P[lo + k].mx);
+            right_area[k] = sahArea(mn, mx);
+        }
+        float lmn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lmx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = 1; k < n; k++) {
+            sahUnion(lmn, lmx, P[lo + k - 1].mn, P[lo + k - 1].mx);
+            const double cost = (double)sahArea(lmn, lmx) * (double)k + (double)right_area[k] * (double)(n - k);
+            if (cost < best_cost) {
+                best_cost = cost;
+                best_axis = axis;
+                best_i = lo + k;
+            }
+        }
+    }
+    std::sort(P.begin() + lo, P.begin() + hi, [best_axis](const SahPrim& x, const SahPrim& y) {
+        return x.c[best_axis] < y.c[best_axis] || (x.c[best_axis] == y.c[best_axis] && x.ref < y.ref);
+    });
+    const size_t range[2][2] = {{lo, best_i}, {best_i, hi}};
+    uint32_t refs[2], needs[2] = {0, 0};
+    float box[2][6];
+    for (int k = 0; k < 2; k++) {
+        const size_t a = range[k][0], b = range[k][1];
+        float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t i = a; i < b; i++) sahUnion(mn, mx, P[i].mn, P[i].mx);
+        for (int q = 0; q < 3; q++) {
+            box[k][q] = mn[q];
+            box[k][3 + q] = mx[q];
+        }
+        refs[k] = b - a == 1 ? P[a].ref : sahBuild(L, P, a, b, out, needs[k], depth + 1);
+    }
+    DNode& d = out[idx];
+    for (int k = 0; k < 2; k++) {
+        float* f = k == 0 ? d.a : d.b;
+        (k == 0 ? d.ref_a : d.ref_b) = refs[k];
+        if ((refs[k] >> KIND_SHIFT) == DK_SPHERE) {
+            const DSphere& sp = L.sph[refs[k] & INDEX_MASK];
+            f[0] = sp.c0[0]; f[1] = sp.c0[1]; f[2] = sp.c0[2]; f[3] = sp.r;
+            f[4] = sp.dc[0]; f[5] = sp.dc[1]; f[6] = sp.dc[2];
+        } else {
+            for (int q = 0; q < 6; q++) f[q] = box[k][q];
+            f[6] = 0.0f;
+        }
+    }
+    const bool ia = (refs[0] >> KIND_SHIFT) == DK_BVH, ib = (refs[1] >> KIND_SHIFT) == DK_BVH;
+    need = (ia && ib) ? 1 + std::max(needs[0], needs[1]) : (ia ? needs[0] : (ib ? needs[1] : 0u));
+    return mkref(DK_BVH, idx);
+}
+
+// leaves of the reference tree left to right
+void inorderLeaves(const HostLayout& L, uint32_t ref, std::vector<uint32_t>& out) {
+    if ((ref >> KIND_SHIFT) == DK_BVH) {
+        inorderLeaves(L, L.bvh[ref & INDEX_MASK].left, out);
+        inorderLeaves(L, L.bvh[ref & INDEX_MASK].right, out);
+    } else {
+        out.push_back(ref);
+    }
+}
+
+// Replace L.node / L.bvh_root by the SAH tree; false (reference tree kept)
+// when the leaves are not numbered in left-to-right order (a shared subtree).
+bool rebuildSah(HostLayout& L) {
+    std::vector<uint32_t> leaves;
+    inorderLeaves(L, L.bvh_root, leaves);
+    if (leaves.size() < 2) return false;
+    for (size_t i = 1; i < leaves.size(); i++)
+        if ((leaves[i] & INDEX_MASK) <= (leaves[i - 1] & INDEX_MASK)) return false;
+    std::vector<SahPrim> P(leaves.size());
+    for (size_t i = 0; i < leaves.size(); i++) {
+        const DSphere& sp = L.sph[leaves[i] & INDEX_MASK];
+        SahPrim& q = P[i];
+        for (int a = 0; a < 3; a++) {
+            // the box every center(time), time in [0, 1], stays in (boxOf)
+            const float c1 = sp.c0[a] + sp.dc[a];
+            q.mn[a] = std::min(sp.c0[a], c1) - sp.r;
+            q.mx[a] = std::max(sp.c0[a], c1) + sp.r;
+            q.c[a] = 0.5f * (q.mn[a] + q.mx[a]);
+        }
+        q.ref = leaves[i];
+    }
+    std::vector<DNode> nodes;
+    uint32_t need = 0;
+    const uint32_t root = sahBuild(L, P, 0, P.size(), nodes, need, 0);
+    L.node.swap(nodes);
+    L.bvh_root = root;
+    L.stack_need = need;
+    return true;
+}
+
 // true when everything below `ref` is BvhNodes and spheres
 bool onlyBvhSpheres(const HostLayout& L, uint32_t ref, int depth = 0) {
     const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
@@ -1346,6 +1507,8 @@ int buildLayout(const rtow_scene& s, HostLayout& L) {
                     }
                 }
             }
+            const char* tree = std::getenv("RTOW_BVH");
+            if (!(tree && std::string(tree) == "ref") && (L.bvh_root >> KIND_SHIFT) == DK_BVH) rebuildSah(L);
         }
     }
     for (uint32_t i = 0; i < s.n_materials; i++) {

@@ -24,7 +24,7 @@ def main():
     import torch
 
     torch.cuda.init()
-    # each variant: path/to/lib.so[:ENV=VAL[,ENV=VAL]] (env applied when its contexts are created)
+    # each variant: path/to/lib.so[:ENV=VAL[,ENV=VAL]] (env applied while its contexts are created and the scene uploaded)
     specs = [a for a in sys.argv[1:] if ".so" in a]
     libs = [a.split(":")[0] for a in specs]
     envs = [dict(kv.split("=") for kv in a.split(":")[1].split(",")) if ":" in a else {} for a in specs]
@@ -40,12 +40,12 @@ def main():
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             ctx = m.Context(0)
+            ctx.upload(sc)  # scene-layout knobs (RTOW_BVH) are read at upload
             for k, v in saved.items():
                 if v is None:
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
-            ctx.upload(sc)
             runs.append((m, sc, ctx, m.camera_main(W, H), m.params(W, H, s, seed=1)))
         imgs = [r[2].render(r[3], r[4], linear=True)[1] for r in runs]
         same = all((im == imgs[0]).all() for im in imgs)
