@@ -204,3 +204,111 @@ def rms(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+# ---- editing flattened scenes (tie / edge-case tests) ----------------------
+HIT_SPHERE, HIT_MOVING_SPHERE, HIT_TRANSLATE, HIT_BVH_NODE = 1, 2, 7, 11
+
+
+def scene_dict(scene):
+    """A library-owned rtow.Scene as a dict of numpy arrays (via RTOWSCN1)."""
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "s.scn")
+        scene.save(p)
+        return load_scene(p)
+
+
+def hitable_box(h, i):
+    """Bounding box of hitable i the way the reference computes it
+    (sphere.h:71-74, 120-127; bvhNode.h:58 union of the children)."""
+    e = h[i]
+    if e["kind"] == HIT_SPHERE:
+        c, r = e["f"][:3].astype(np.float32), np.float32(e["f"][3])
+        return c - r, c + r
+    if e["kind"] == HIT_MOVING_SPHERE:
+        c0, c1, r = e["f"][:3], e["f"][3:6], np.float32(e["f"][8])
+        return np.minimum(c0, c1) - r, np.maximum(c0, c1) + r
+    if e["kind"] == HIT_BVH_NODE:
+        a0, a1 = hitable_box(h, e["a"])
+        b0, b1 = hitable_box(h, e["b"])
+        return np.minimum(a0, b0), np.maximum(a1, b1)
+    raise ValueError(f"no box for kind {e['kind']}")
+
+
+def refresh_bvh_boxes(d):
+    """Recompute every BvhNode's stored box from its children (after moving
+    leaves), bottom-up, in place."""
+    h = d["hitables"]
+    for i in range(len(h)):
+        if h[i]["kind"] == HIT_BVH_NODE:
+            lo, hi = hitable_box(h, i)
+            h[i]["f"][:3] = lo
+            h[i]["f"][3:6] = hi
+
+
+def bvh_leaves_in_order(d):
+    """Hitable indices of the leaves under the root's BvhNode, left to right."""
+    h = d["hitables"]
+    i = d["root"]
+    while h[i]["kind"] == HIT_TRANSLATE:
+        i = h[i]["a"]
+    out = []
+
+    def walk(k):
+        if h[k]["kind"] == HIT_BVH_NODE:
+            walk(h[k]["a"])
+            if h[k]["b"] != h[k]["a"]:
+                walk(h[k]["b"])
+        else:
+            out.append(int(k))
+
+    walk(i)
+    return out
+
+
+class ArrayScene:
+    """An edited scene dict behind the `view_ptr` interface rtow.Context.upload
+    and oracle_render take."""
+
+    def __init__(self, d):
+        self.arrays = SceneArrays(d)
+
+    @property
+    def view_ptr(self):
+        return ctypes.addressof(self.arrays.view)
+
+
+def tie_scene(n=100):
+    """random_ned with an exact duplicate of a large sphere: leaf X (earlier in
+    the reference tree's left-to-right order) is moved onto leaf Y's center and
+    radius, boxes refreshed.  Every ray that meets one meets both at the same
+    t; BvhNode::hit (bvhNode.h:74-77) hands the tie to the later leaf.
+    Returns (dict, earlier leaf, later leaf)."""
+    import rtow
+
+    d = scene_dict(rtow.Scene.build("random_ned", n=n, image="none"))
+    h = d["hitables"]
+    leaves = bvh_leaves_in_order(d)
+    big = [k for k in leaves if h[k]["kind"] == HIT_SPHERE and 0.45 < h[k]["f"][3] < 10]
+    small = [k for k in leaves if h[k]["kind"] == HIT_SPHERE and h[k]["f"][3] < 0.3]
+    # Y: the large sphere nearest the main camera among those on screen
+    cam = rtow.camera_main(64, 36)
+    org, llc = np.array(cam.origin[:]), np.array(cam.lower_left_corner[:])
+    hor, ver = np.array(cam.horizontal[:]), np.array(cam.vertical[:])
+    off = h[d["root"]]["f"][:3] if h[d["root"]]["kind"] == HIT_TRANSLATE else np.zeros(3)
+
+    def screen(k):
+        c = h[k]["f"][:3].astype(np.float64) + off
+        u, v, s = np.linalg.solve(np.stack([hor, ver, -(c - org)], axis=1), org - llc)
+        return u, v, np.linalg.norm(c - org)
+
+    on = [(screen(k)[2], k) for k in big if all(0.15 < q < 0.85 for q in screen(k)[:2])]
+    y = min(on)[1]
+    x = small[-1] if leaves.index(small[-1]) > leaves.index(y) else small[0]
+    h[x]["f"][:4] = h[y]["f"][:4]
+    refresh_bvh_boxes(d)
+    pos = {k: leaves.index(k) for k in (x, y)}
+    early, late = sorted((x, y), key=lambda k: pos[k])
+    return d, early, late
