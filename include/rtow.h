@@ -249,6 +249,17 @@ int rtow_camera_main(uint32_t width, uint32_t height, rtow_camera* out);
 /* Fill an RGB8 image with the synthetic "earth" stand-in. */
 void rtow_synthetic_image(uint32_t nx, uint32_t ny, uint8_t* rgb);
 
+/* ---- frame output ------------------------------------------------------------ */
+/* The reference's BMP file (WINDIBBitmap::writeBMPToFile, winDIBbitmap.cpp:
+ * 20-168, as main.cpp:774 calls it with the BGRA frame and 32 bpp): 54-byte
+ * header with a POSITIVE height, then the buffer rows in order, each padded
+ * to 4 bytes, so viewers show the top-down frame flipped exactly as the
+ * reference's test.bmp.  size_bytes must be width*height*bits_per_pixel/8. */
+int rtow_write_bmp(const char* path, const uint8_t* pixels, uint64_t size_bytes, uint32_t width,
+                   uint32_t height, uint32_t bits_per_pixel);
+/* Binary PPM (P6, RGB, top row first) of a BGRA frame, for inspection. */
+int rtow_write_ppm(const char* path, const uint8_t* bgra, uint32_t width, uint32_t height);
+
 /* ---- device path ------------------------------------------------------------ */
 typedef struct rtow_context rtow_context;
 
@@ -263,6 +274,21 @@ int rtow_context_destroy(rtow_context* ctx);
 int rtow_scene_check(const rtow_scene* scene, uint32_t* stack_need, uint32_t* chain_need);
 /* Convert the scene graph to the device layout and copy it to HBM. */
 int rtow_scene_upload(rtow_context* ctx, const rtow_scene* scene);
+
+/* Acceleration tree the device traverses for a scene made of BvhNodes and
+ * spheres only (taking effect at the next rtow_scene_upload).  The closest
+ * hit does not depend on it: exact ties are settled by the reference tree's
+ * leaf order (BvhNode::hit, bvhNode.h:74-77) either way, so both give the
+ * same frame.  SAH (default): a surface-area-heuristic tree rebuilt over the
+ * same spheres.  REFERENCE: the reference's own random-axis median-split tree
+ * (bvhNode.h:25-59).  Other scenes always use the reference tree.  The
+ * environment variable RTOW_BVH=ref|sah overrides the default at context
+ * creation. */
+enum {
+    RTOW_TREE_SAH = 0,
+    RTOW_TREE_REFERENCE = 1
+};
+int rtow_context_set_tree(rtow_context* ctx, int tree);
 
 /* Drop-in for main.cpp:932-996 on one GPU: render every pixel, write the BGRA
  * frame (host memory, W*H*4, alpha 0) and, if linear_out is not NULL, the

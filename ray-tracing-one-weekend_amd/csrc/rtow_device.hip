@@ -1447,7 +1447,7 @@ bool textureNeedsUv(const rtow_scene& s, uint32_t ti, int guard = 0) {
     return false;
 }
 
-int buildLayout(const rtow_scene& s, HostLayout& L) {
+int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     if (s.root >= s.n_hitables || !s.hitables || !s.materials || !s.textures || !s.perlin)
         return set_error(RTOW_E_INVALID, "incomplete scene");
     for (uint32_t i = 0; i < s.n_hitables; i++) {
@@ -1507,8 +1507,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L) {
                     }
                 }
             }
-            const char* tree = std::getenv("RTOW_BVH");
-            if (!(tree && std::string(tree) == "ref") && (L.bvh_root >> KIND_SHIFT) == DK_BVH) rebuildSah(L);
+            if (tree == RTOW_TREE_SAH && (L.bvh_root >> KIND_SHIFT) == DK_BVH) rebuildSah(L);
         }
     }
     for (uint32_t i = 0; i < s.n_materials; i++) {
@@ -1570,6 +1569,7 @@ struct rtow_context {
     int waves = 4;  // trace-kernel occupancy variant (RTOW_TRACE_WAVES; 4 measured best, tools/probe.py)
     int profile = 0;  // RTOW_PROFILE=1: instrumented trace kernel, counters printed to stderr
     int lds_nodes = 1;  // simple-scene BVH staged in LDS when it fits (RTOW_LDS_NODES=0 disables; +11%, tools/ab.py)
+    int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     // scene
@@ -1807,6 +1807,7 @@ int rtow_context_create(int device, rtow_context** out) {
     if (const char* w = std::getenv("RTOW_TRACE_WAVES")) c->waves = std::atoi(w);
     if (const char* pr = std::getenv("RTOW_PROFILE")) c->profile = std::atoi(pr);
     if (const char* ln = std::getenv("RTOW_LDS_NODES")) c->lds_nodes = std::atoi(ln);
+    if (const char* tr = std::getenv("RTOW_BVH")) c->tree = std::string(tr) == "ref" ? RTOW_TREE_REFERENCE : RTOW_TREE_SAH;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
@@ -1842,10 +1843,17 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
     return RTOW_OK;
 }
 
+int rtow_context_set_tree(rtow_context* c, int tree) {
+    if (!c) return set_error(RTOW_E_INVALID, "NULL context");
+    if (tree != RTOW_TREE_SAH && tree != RTOW_TREE_REFERENCE) return set_error(RTOW_E_INVALID, "unknown tree");
+    c->tree = tree;
+    return RTOW_OK;
+}
+
 int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     if (!c || !s) return set_error(RTOW_E_INVALID, "NULL argument");
     HostLayout L;
-    int rc = buildLayout(*s, L);
+    int rc = buildLayout(*s, L, c->tree);
     if (rc) return rc;
     std::vector<uint8_t> blob;
     size_t o_bvh = pushBlob(blob, L.bvh), o_node = pushBlob(blob, L.node), o_sph = pushBlob(blob, L.sph);

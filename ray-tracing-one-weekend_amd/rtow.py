@@ -102,6 +102,9 @@ def lib():
         "rtow_context_create": ([i32, ctypes.POINTER(vp)], i32),
         "rtow_context_destroy": ([vp], i32),
         "rtow_scene_upload": ([vp, vp], i32),
+        "rtow_context_set_tree": ([vp, i32], i32),
+        "rtow_write_bmp": ([ctypes.c_char_p, vp, ctypes.c_uint64, u32, u32, u32], i32),
+        "rtow_write_ppm": ([ctypes.c_char_p, vp, u32, u32], i32),
         "rtow_render": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)], i32),
         "rtow_render_tiles_device": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, vp,
                                       ctypes.POINTER(Stats)], i32),
@@ -156,6 +159,22 @@ def synthetic_image(nx, ny):
     out = np.zeros((ny, nx, 3), np.uint8)
     lib().rtow_synthetic_image(nx, ny, out.ctypes.data)
     return out
+
+
+def write_bmp(path, pixels, width, height, bits_per_pixel=32):
+    """The reference's BMP writer (winDIBbitmap.cpp:20-168) on a frame buffer."""
+    buf = np.ascontiguousarray(pixels, dtype=np.uint8)
+    check(lib().rtow_write_bmp(path.encode(), buf.ctypes.data, buf.nbytes, width, height, bits_per_pixel),
+          "rtow_write_bmp")
+
+
+def write_ppm(path, bgra):
+    """bgra: [H, W, 4] uint8 frame (top row first) -> binary PPM."""
+    buf = np.ascontiguousarray(bgra, dtype=np.uint8)
+    check(lib().rtow_write_ppm(path.encode(), buf.ctypes.data, buf.shape[1], buf.shape[0]), "rtow_write_ppm")
+
+
+TREES = {"sah": 0, "reference": 1}
 
 
 class Scene:
@@ -227,6 +246,11 @@ class Context:
         h = ctypes.c_void_p()
         check(lib().rtow_context_create(device, ctypes.byref(h)), "rtow_context_create")
         self._h = h
+
+    def set_tree(self, tree):
+        """'sah' (default) or 'reference': the tree the next upload builds for
+        BvhNode+sphere scenes (the frame is the same either way)."""
+        check(lib().rtow_context_set_tree(self._h, TREES[tree]), "rtow_context_set_tree")
 
     def upload(self, scene):
         check(lib().rtow_scene_upload(self._h, scene.view_ptr), "rtow_scene_upload")

@@ -167,3 +167,22 @@ def test_full_frame_every_pixel_against_oracle(gpu_ctx):
     # measured (round 1): rms ~1-2e-5 per channel, 11 of 2,073,600 pixels > 1e-3
     assert int((d > 1e-3).sum()) <= 1e-5 * W * H
     assert (rms <= RMS_TOL).all()  # even unscaled at 8 spp
+
+
+@pytest.mark.parametrize("scene,n", [("random_ned", 487), ("random_ned", 100), ("three_sphere", 0)])
+def test_tree_does_not_change_the_frame(scene, n):
+    """The SAH tree (default) and the reference's own BvhNode tree give the
+    same frame bit for bit: the closest hit is a property of the leaves, and
+    exact ties follow the reference's leaf order in both."""
+    W, H, spp = 96, 54, 16
+    sc = rtow.Scene.build(scene, n=max(n, 1), image="synthetic")
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, spp, seed=17)
+    frames = []
+    for tree in ("sah", "reference"):
+        ctx = rtow.Context(0)
+        ctx.set_tree(tree)
+        ctx.upload(sc)
+        frames.append(ctx.render(cam, p)[1])
+        ctx.close()
+    assert np.array_equal(frames[0].view(np.uint32), frames[1].view(np.uint32))
