@@ -215,7 +215,9 @@ enum {
     RTOW_SCENE_THREE_SPHERE = 1,  /* config 1: three Lambertian spheres (composed) */
     RTOW_SCENE_RANDOM_NED = 2,    /* randomScene_NED scenes.h:122-218, n parameterised */
     RTOW_SCENE_CORNELL_NED = 3,   /* cornellBox_NED scenes.h:355-483 */
-    RTOW_SCENE_CORNELL_SMOKE = 4  /* cornellBox_NED + smoke box of scenes.h:461-470 */
+    RTOW_SCENE_CORNELL_SMOKE = 4, /* cornellBox_NED + smoke box of scenes.h:461-470 */
+    RTOW_SCENE_FINAL_NED = 5      /* config 5: book 2's final scene composed from the reference's
+                                     classes in NED; root Translate (600,-278,278) */
 };
 
 enum {
@@ -305,6 +307,16 @@ int rtow_render(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
 int rtow_render_tiles_device(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
                              void* d_bgra_slab, void* d_linear_slab, void* stream,
                              rtow_stats* stats);
+
+/* Diagnostic: render the frame with the segment-recording kernel and return
+ * the path of ONE sample (pixel x, y of the top-down frame, sample index):
+ * per color() call RTOW_DEBUG_SEG_FLOATS floats {hit, depth, t, p.xyz (the
+ * ray direction on a miss), n.xyz, material, random draws so far, 1}; the
+ * oracle's rtow_oracle_trace_sample writes the same records. */
+#define RTOW_DEBUG_SEG_FLOATS 12
+int rtow_debug_trace_sample(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p, uint32_t x,
+                            uint32_t y, uint32_t sample, float* out, uint32_t max_segments,
+                            uint32_t* n_segments);
 
 /* Scatter the gathered slabs of all `world` ranks (rank-major, each
  * rtow_rank_tile_count(...) * 64 pixels; equal-size padding allowed via

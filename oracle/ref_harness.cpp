@@ -23,7 +23,7 @@
 //   ref_harness render <scene> <W> <H> <spp> <out_prefix> [opts]
 //       writes <out_prefix>.lin (W*H*3 float32, framebuffer order) and
 //       <out_prefix>.bgra (W*H*4 bytes, main.cpp:982-989)
-// scenes: three_sphere | random_ned | cornell | cornell_smoke
+// scenes: three_sphere | random_ned | cornell | cornell_smoke | final_ned
 // opts:   --n N  --scene-seed S  --seed S  --threads T  --cwd DIR
 // The scene stream seed is read from RTOW_SCENE_SEED (environment) because the
 // Perlin tables are drawn during static initialisation (noise.h:112-116),
@@ -342,6 +342,63 @@ static Hitable* cornellSmokeNed() {
     return l;
 }
 
+// Config 5: book 2's final scene ("The Next Week", final chapter) has no
+// reference function; composed here from reference classes and transcribed to
+// the reference's NED frame: NED (x north, y east, z down) = (book z, book x,
+// -book y).  The book rotates its sphere cloud about its vertical axis, which
+// is NED z, for which the reference has no class: RotateY (about NED y, the
+// reference's only rotation) takes its place.  Every random draw is sequenced
+// explicitly.  main.cpp-style root Translate puts the book's look-at point
+// (278, 278, 0) straight ahead of the main camera, 600 units out.
+static Hitable* finalSceneNed(bool* usedImage) {
+    Hitable** list = new Hitable*[16];
+    Hitable** boxes = new Hitable*[400];
+    Hitable** cloud = new Hitable*[1000];
+    Material* white = new Lambertian(new ConstantTexture(vec3(0.73, 0.73, 0.73)));
+    Material* ground = new Lambertian(new ConstantTexture(vec3(0.48, 0.83, 0.53)));
+    int b = 0;
+    for (int i = 0; i < 20; i++) {
+        for (int j = 0; j < 20; j++) {
+            float w = 100;
+            float x0 = -1000 + i * w;
+            float z0 = -1000 + j * w;
+            float x1 = x0 + w;
+            float y1 = 100 * (U() + 0.01);
+            float z1 = z0 + w;
+            boxes[b++] = new Box(vec3(z0, x0, -y1), vec3(z1, x1, 0), ground);
+        }
+    }
+    int l = 0;
+    list[l++] = new BvhNode(boxes, b, 0, 1);
+    Material* light = new DiffuseLight(new ConstantTexture(vec3(7, 7, 7)));
+    list[l++] = new XYRectangle(147, 412, 123, 423, -554, light);
+    vec3 center(200, 400, -400);
+    list[l++] = new MovingSphere(center, center + vec3(0, 30, 0), 0, 1, 50,
+                                 new Lambertian(new ConstantTexture(vec3(0.7, 0.3, 0.1))));
+    list[l++] = new Sphere(vec3(45, 260, -150), 50, new Dielectric(1.5));
+    list[l++] = new Sphere(vec3(145, 0, -150), 50, new Metal(vec3(0.8, 0.8, 0.9), 10.0));
+    Hitable* boundary = new Sphere(vec3(145, 360, -150), 70, new Dielectric(1.5));
+    list[l++] = boundary;
+    list[l++] = new ConstantMedium(boundary, 0.2, new ConstantTexture(vec3(0.2, 0.4, 0.9)));
+    boundary = new Sphere(vec3(0, 0, 0), 5000, new Dielectric(1.5));
+    list[l++] = new ConstantMedium(boundary, 0.0001, new ConstantTexture(vec3(1.0, 1.0, 1.0)));
+    int nx = 0, ny = 0, nn = 0;
+    unsigned char* texData = stbi_load("./input_images/1_earth_8k.jpg", &nx, &ny, &nn, 0);
+    *usedImage = texData != nullptr;
+    Material* emat = texData ? (Material*)new Lambertian(new ImageTexture(texData, nx, ny))
+                             : (Material*)new Dielectric(1.5);
+    list[l++] = new Sphere(vec3(400, 400, -200), 100, emat);
+    list[l++] = new Sphere(vec3(300, 220, -280), 80, new Lambertian(new NoiseTexture(true, 0.1f)));
+    for (int j = 0; j < 1000; j++) {
+        double bx = U();
+        double by = U();
+        double bz = U();
+        cloud[j] = new Sphere(vec3(165 * bz, 165 * bx, -165 * by), 10, white);
+    }
+    list[l++] = new Translate(new RotateY(new BvhNode(cloud, 1000, 0.0, 1.0), 15), vec3(395, -100, -270));
+    return new HitableList(list, l);
+}
+
 struct Opts {
     int n = 100;
     uint64_t seed = 1;
@@ -369,6 +426,10 @@ static Hitable* buildWorld(const std::string& name, const Opts& o) {
     if (name == "cornell") return new Translate(cornellBox_NED(), vec3(800, 0, 0));
     if (name == "cornell_smoke") return new Translate(cornellSmokeNed(), vec3(800, 0, 0));
     if (name == "three_sphere") return threeSphereNed();
+    if (name == "final_ned") {
+        bool used;
+        return new Translate(finalSceneNed(&used), vec3(600, -278, 278));
+    }
     std::fprintf(stderr, "unknown scene %s\n", name.c_str());
     std::exit(2);
 }

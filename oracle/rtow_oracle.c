@@ -48,6 +48,8 @@ typedef struct { uint64_t key; uint32_t ctr; } rng_t;
 typedef struct {
     const rtow_scene* s;
     rtow_oracle_counters c;
+    float* trace; /* rtow_oracle_trace_sample: segment records, or NULL */
+    uint32_t trace_max, trace_n;
 } ctx_t;
 
 static inline double unif(ctx_t* cx, rng_t* g) {
@@ -490,7 +492,24 @@ static v3 color(ctx_t* cx, rng_t* g, const rtow_params* P, const ray_t* r, int d
     hitrec rec;
     memset(&rec, 0, sizeof rec);
     cx->c.segments++;
-    if (hit(cx, g, cx->s->root, r, 0.001f, FLT_MAX, &rec)) {
+    const int hit_any = hit(cx, g, cx->s->root, r, 0.001f, FLT_MAX, &rec);
+    if (cx->trace && cx->trace_n < cx->trace_max) {
+        float* o = cx->trace + (size_t)cx->trace_n * RTOW_DEBUG_SEG_FLOATS;
+        o[0] = hit_any ? 1.0f : 0.0f;
+        o[1] = (float)depth;
+        o[2] = hit_any ? rec.t : 0.0f;
+        o[3] = hit_any ? rec.p.x : r->d.x;
+        o[4] = hit_any ? rec.p.y : r->d.y;
+        o[5] = hit_any ? rec.p.z : r->d.z;
+        o[6] = hit_any ? rec.n.x : 0.0f;
+        o[7] = hit_any ? rec.n.y : 0.0f;
+        o[8] = hit_any ? rec.n.z : 0.0f;
+        o[9] = hit_any ? (float)rec.mat : -1.0f;
+        o[10] = (float)g->ctr;
+        o[11] = 1.0f;
+        cx->trace_n++;
+    }
+    if (hit_any) {
         const rtow_material* m = &cx->s->materials[rec.mat];
         ray_t scattered;
         v3 atten;
@@ -513,12 +532,9 @@ static v3 color(ctx_t* cx, rng_t* g, const rtow_params* P, const ray_t* r, int d
 }
 
 /* ---- render loop (main.cpp:932-996 + camera.h:123-135) ------------------- */
-static v3 render_pixel(ctx_t* cx, const rtow_camera* C, const rtow_params* P, uint32_t fb_index) {
+static v3 sample_color(ctx_t* cx, const rtow_camera* C, const rtow_params* P, int column, int row, uint32_t s) {
     const uint32_t W = P->width, H = P->height;
-    uint32_t x = fb_index % W, y = fb_index / W;
-    int column = (int)x, row = (int)(H - 1 - y);
-    v3 out = mk(0, 0, 0);
-    for (uint32_t s = 0; s < P->spp; s++) {
+    {
         rng_t g;
         g.key = rtow_sample_key(P->seed, (uint32_t)row * W + (uint32_t)column, s);
         g.ctr = 0;
@@ -536,11 +552,21 @@ static v3 render_pixel(ctx_t* cx, const rtow_camera* C, const rtow_params* P, ui
                       ld3(C->origin)),
                   offset);
         r.time = time;
-        out = add(out, color(cx, &g, P, &r, 0));
+        v3 c = color(cx, &g, P, &r, 0);
         cx->c.samples++;
         uint64_t nd = cx->c.draws - d0;
         if (nd > cx->c.max_draws_per_sample) cx->c.max_draws_per_sample = nd;
+        (void)H;
+        return c;
     }
+}
+
+static v3 render_pixel(ctx_t* cx, const rtow_camera* C, const rtow_params* P, uint32_t fb_index) {
+    const uint32_t W = P->width, H = P->height;
+    uint32_t x = fb_index % W, y = fb_index / W;
+    int column = (int)x, row = (int)(H - 1 - y);
+    v3 out = mk(0, 0, 0);
+    for (uint32_t s = 0; s < P->spp; s++) out = add(out, sample_color(cx, C, P, column, row, s));
     float k = (float)(1.0 / (float)P->spp); /* vec3.h:133-139 */
     return mk(out.x * k, out.y * k, out.z * k);
 }
@@ -646,6 +672,21 @@ int rtow_oracle_render(const rtow_scene* scene, const rtow_camera* cam, const rt
     if (!p) return RTOW_E_INVALID;
     return rtow_oracle_render_pixels(scene, cam, p, NULL, p->width * p->height, threads, lin, bgra,
                                      counters);
+}
+
+int rtow_oracle_trace_sample(const rtow_scene* scene, const rtow_camera* cam, const rtow_params* p, uint32_t x,
+                             uint32_t y, uint32_t sample, float* out, uint32_t max_segments, uint32_t* n_segments) {
+    int rc = validate(scene, p);
+    if (rc) return rc;
+    if (!cam || !out || x >= p->width || y >= p->height || sample >= p->spp) return RTOW_E_INVALID;
+    ctx_t cx;
+    memset(&cx, 0, sizeof cx);
+    cx.s = scene;
+    cx.trace = out;
+    cx.trace_max = max_segments;
+    (void)sample_color(&cx, cam, p, (int)x, (int)(p->height - 1 - y), sample);
+    if (n_segments) *n_segments = cx.trace_n;
+    return 0;
 }
 
 /* ---- scene file loader ("RTOWSCN1") ---------------------------- */

@@ -58,6 +58,11 @@ int rtow_oracle_render_pixels(const rtow_scene* scene, const rtow_camera* cam, c
 int rtow_oracle_render(const rtow_scene* scene, const rtow_camera* cam, const rtow_params* p,
                        int threads, float* lin, uint8_t* bgra, rtow_oracle_counters* counters);
 
+/* The path of one sample (pixel x, y of the top-down frame): per color() call
+ * RTOW_DEBUG_SEG_FLOATS floats, the records rtow_debug_trace_sample writes. */
+int rtow_oracle_trace_sample(const rtow_scene* scene, const rtow_camera* cam, const rtow_params* p, uint32_t x,
+                             uint32_t y, uint32_t sample, float* out, uint32_t max_segments, uint32_t* n_segments);
+
 #ifdef __cplusplus
 }
 #endif

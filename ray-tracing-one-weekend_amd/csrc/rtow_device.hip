@@ -97,6 +97,10 @@ struct DevParams {
     float sky_gain, gi_gain;
     uint64_t seed;
     uint32_t n_items;
+    // rtow_debug_trace_sample: the one (column, row, sample) whose segments
+    // the DBG kernel records (RTOW_DEBUG_SEG_FLOATS floats each) into dbg_out
+    uint32_t dbg_col, dbg_row, dbg_sample, dbg_max;
+    float* dbg_out;
 };
 
 struct Rec {
@@ -249,8 +253,7 @@ __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, 
 // the nearer wins and an exact tie goes to the later leaf of the reference
 // tree, i.e. the larger sphere index (see rebuildSah).  `bt`/`best` is the
 // record so far.  The far root is only evaluated when the near one is <= tmin.
-__device__ __forceinline__ bool sph_closer(F3 center, float radius, const Ray& r, float a, float tmin, float bt,
-                                           uint32_t best, uint32_t ref, float& t) {
+__device__ __forceinline__ bool sph_root(F3 center, float radius, const Ray& r, float a, float tmin, float& t) {
     const F3 oc = sub(r.o, center);
     const float b = dot(r.d, oc);
     const float c = dot(oc, oc) - radius * radius;
@@ -259,12 +262,15 @@ __device__ __forceinline__ bool sph_closer(F3 center, float radius, const Ray& r
         const float sq = sqrtf(disc);
         float root = (-b - sq) / a;
         if (!(root < FLT_MAX && root > tmin)) root = (-b + sq) / a;
-        if (root < FLT_MAX && root > tmin && (root < bt || (root == bt && ref > best))) {
-            t = root;
-            return true;
-        }
+        t = root;
+        return root < FLT_MAX && root > tmin;
     }
     return false;
+}
+
+__device__ __forceinline__ bool sph_closer(F3 center, float radius, const Ray& r, float a, float tmin, float bt,
+                                           uint32_t best, uint32_t ref, float& t) {
+    return sph_root(center, radius, r, a, tmin, t) && (t < bt || (t == bt && ref > best));
 }
 
 template <bool UNIT_TIME>
@@ -295,6 +301,16 @@ struct Prof {
     uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
     unsigned long long cyc_trav, cyc_other;  // wave cycles (s_memtime) in traversal / everything else
 };
+// General scenes: does leaf `cand`, hit at exactly the t of the current best
+// leaf `best`, take the record in the reference?  (assignTieKeys)
+__device__ __forceinline__ unsigned long long leaf_key(const DevScene& S, uint32_t ref) {
+    const uint32_t k = ref >> KIND_SHIFT, i = ref & INDEX_MASK;
+    return k == DK_SPHERE ? S.sph_key[i] : (k == DK_RECT ? S.rect_key[i] : (k == DK_MEDIUM ? S.med_key[i] : 0ull));
+}
+__device__ __noinline__ bool wins_tie(const DevScene& S, uint32_t cand, uint32_t best) {
+    return (best >> KIND_SHIFT) == DK_NONE || leaf_key(S, cand) > leaf_key(S, best);
+}
+
 __device__ __forceinline__ bool first_active_lane() {
     const unsigned long long m = __ballot(1);
     return (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1);
@@ -310,6 +326,7 @@ template <bool UNIT_TIME, int STACK>
 __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
                                              float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
                                              uint32_t& overflow) {
+    // `best`: in, the current closest leaf; out, the winner of this step's spheres
     const DBvh* n = S.bvh + idx;
     const float4 xs = reinterpret_cast<const float4*>(n)[0];
     const float4 ys = reinterpret_cast<const float4*>(n)[1];
@@ -322,14 +339,18 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
     const bool rleaf = (lr.y >> KIND_SHIFT) == DK_SPHERE;
     if (hr && rleaf) {
         float t;
-        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.y & INDEX_MASK)), r, a, tmin, bt, t)) {
+        const Sph sp1 = load_sph(S.sph + (lr.y & INDEX_MASK));
+        if (sph_root(sph_center<UNIT_TIME>(sp1, r.time), sp1.r, r, a, tmin, t) &&
+            (t < bt || (t == bt && wins_tie(S, lr.y, best)))) {
             bt = t;
             best = lr.y;
         }
     }
     if (hl && lleaf) {
         float t;
-        if (sph_t<UNIT_TIME>(load_sph(S.sph + (lr.x & INDEX_MASK)), r, a, tmin, bt, t)) {
+        const Sph sp0 = load_sph(S.sph + (lr.x & INDEX_MASK));
+        if (sph_root(sph_center<UNIT_TIME>(sp0, r.time), sp0.r, r, a, tmin, t) &&
+            (t < bt || (t == bt && wins_tie(S, lr.x, best)))) {
             bt = t;
             best = lr.x;
         }
@@ -480,11 +501,12 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
         uint32_t kind = cur >> KIND_SHIFT;
         const uint32_t idx = cur & INDEX_MASK;
         if (kind == DK_BVH) {
-            uint32_t b = mkref(DK_NONE, 0);
+            const uint32_t before = found ? best.prim : mkref(DK_NONE, 0);
+            uint32_t b = before;
             const uint32_t nxt = S.unit_time
                                      ? bvh_step<true, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow)
                                      : bvh_step<false, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow);
-            if ((b >> KIND_SHIFT) != DK_NONE) {
+            if (b != before) {
                 take_best(best, b, ch, cn);
                 found = true;
             }
@@ -495,14 +517,17 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
         } else if (kind == DK_SPHERE) {
             float t;
             const Sph s = load_sph(S.sph + idx);
-            if (S.unit_time ? sph_t<true>(s, r, a, tmin, bt, t) : sph_t<false>(s, r, a, tmin, bt, t)) {
+            const F3 c = S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time);
+            if (sph_root(c, s.r, r, a, tmin, t) &&
+                (t < bt || (t == bt && wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0))))) {
                 bt = t;
                 take_best(best, cur, ch, cn);
                 found = true;
             }
         } else if (kind == DK_RECT) {
             float t;
-            if (rect_t(S.rect[idx], r, tmin, bt, t)) {
+            if (rect_t(S.rect[idx], r, tmin, bt, t) &&
+                (t < bt || wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0)))) {
                 bt = t;
                 take_best(best, cur, ch, cn);
                 found = true;
@@ -810,7 +835,7 @@ constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0);
 }
 
-template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false>
+template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
                                                        float4* partial, unsigned long long* counters) {
     Prof prof{0, 0, 0, 0, 0, 0, 0, 0};
@@ -837,6 +862,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     const uint32_t lane = threadIdx.x & 63u;
 
     uint32_t item = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0, overflow = 0;
+    uint32_t nseg_dbg = 0;
     bool need_item = true, need_sample = false;
     F3 acc = f3(0, 0, 0), thr = f3(1, 1, 1);
     Ray ray;
@@ -918,6 +944,27 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             best.n = 0;
             hit = traverse<MODE == 3, STACK>(S, S.root, ray, 0.001f, FLT_MAX, stk, 0, rng, best, overflow);
             if (hit) finalize(S, best.prim, best.t, best.ch, best.n, ray, rec);
+        }
+        if constexpr (DBG) {
+            if (col == P.dbg_col && row == P.dbg_row && s == P.dbg_sample) {
+                const uint32_t k = min(nseg_dbg, P.dbg_max);
+                if (k < P.dbg_max) {
+                    float* o = P.dbg_out + (size_t)k * RTOW_DEBUG_SEG_FLOATS;
+                    o[0] = hit ? 1.0f : 0.0f;
+                    o[1] = (float)depth;
+                    o[2] = hit ? rec.t : 0.0f;
+                    o[3] = hit ? rec.p.x : ray.d.x;
+                    o[4] = hit ? rec.p.y : ray.d.y;
+                    o[5] = hit ? rec.p.z : ray.d.z;
+                    o[6] = hit ? rec.n.x : 0.0f;
+                    o[7] = hit ? rec.n.y : 0.0f;
+                    o[8] = hit ? rec.n.z : 0.0f;
+                    o[9] = hit ? (float)rec.mat : -1.0f;
+                    o[10] = (float)rng.ctr;
+                    o[11] = 1.0f;
+                }
+                nseg_dbg++;
+            }
         }
         bool done = true;
         F3 contrib = f3(0, 0, 0);
@@ -1080,7 +1127,79 @@ struct HostLayout {
     uint32_t root_chain_n = 0;
     uint32_t root_chain[4] = {0, 0, 0, 0};
     uint32_t bvh_root = 0;
+    std::vector<unsigned long long> sph_key, rect_key, med_key;
 };
+
+// ---------------------------------------------------------------------------
+// Exact ties in general scenes.  The reference returns, among the leaves hit
+// at the minimal t, the one its evaluation order leaves in the record:
+// BvhNode::hit hands a tie to the right child (bvhNode.h:74-77); HitableList
+// scans items in order with tmax = the closest so far (hitableList.h:20-38),
+// so a later item takes a tie only if its leaf accepts t == tmax -- the
+// rectangles do (closed interval, xy_rect.h:25), spheres and media do not.
+// Per leaf, along its path from the root, one key component per BvhNode
+// (left 0, right 1) and per list of N items (item j: N + j for a rectangle,
+// N - 1 - j otherwise), packed most significant first: the first component
+// where two keys differ is their lowest common ancestor's, and the larger key
+// is the reference's winner.  Instances add nothing; leaves under a medium
+// boundary are queried for t alone and get no key.  (Not reproduced: a
+// BvhNode ITEM of a list whose box the ray enters exactly at the tied t is
+// culled by AABB::hit's `tmax <= tmin`, so its leaf cannot take the tie.)
+struct KeyComp {
+    uint32_t bits;
+    unsigned long long closed, open;
+};
+
+void assignTieKeys(HostLayout& L, uint32_t ref, std::vector<KeyComp>& path, int depth = 0) {
+    if (depth > 512) return;
+    const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+    auto key = [&](bool closed) {
+        unsigned long long k = 0;
+        uint32_t used = 0;
+        for (const KeyComp& c : path) {
+            if (used + c.bits > 64) break;  // deeper levels: ties there stay with the first found
+            k = (k << c.bits) | (closed ? c.closed : c.open);
+            used += c.bits;
+        }
+        return used ? k << (64 - used) : 0ull;
+    };
+    switch (kind) {
+    case DK_SPHERE:
+        L.sph_key[idx] = key(false);
+        break;
+    case DK_RECT:
+        L.rect_key[idx] = key(true);
+        break;
+    case DK_MEDIUM:
+        L.med_key[idx] = key(false);
+        break;
+    case DK_BVH:
+        for (uint32_t c = 0; c < 2; c++) {
+            path.push_back(KeyComp{1, c, c});
+            assignTieKeys(L, c ? L.bvh[idx].right : L.bvh[idx].left, path, depth + 1);
+            path.pop_back();
+        }
+        break;
+    case DK_LIST: {
+        const DList l = L.list[idx];
+        uint32_t bits = 1;
+        while ((1ull << bits) < 2ull * l.count) bits++;
+        for (uint32_t j = 0; j < l.count; j++) {
+            path.push_back(KeyComp{bits, (unsigned long long)l.count + j, (unsigned long long)l.count - 1 - j});
+            assignTieKeys(L, L.refs[l.first + j], path, depth + 1);
+            path.pop_back();
+        }
+        break;
+    }
+    case DK_TRANSLATE:
+    case DK_ROTY:
+    case DK_FLIP:
+        assignTieKeys(L, L.inst[idx].child, path, depth + 1);
+        break;
+    default:
+        break;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Simple scenes are traversed over a surface-area-heuristic tree rebuilt from
@@ -1549,6 +1668,16 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     if (s.n_texel_bytes) L.texels.assign(s.texels, s.texels + s.n_texel_bytes);
     // keep every array non-empty so each gets a valid device pointer
     if (L.bvh.empty()) L.bvh.push_back(DBvh{});
+    L.sph_key.assign(L.sph.size(), 0ull);
+    L.rect_key.assign(L.rect.size(), 0ull);
+    L.med_key.assign(L.med.size(), 0ull);
+    {
+        std::vector<KeyComp> path;
+        assignTieKeys(L, L.root, path);
+    }
+    if (L.sph_key.empty()) L.sph_key.push_back(0);
+    if (L.rect_key.empty()) L.rect_key.push_back(0);
+    if (L.med_key.empty()) L.med_key.push_back(0);
     if (L.node.empty()) L.node.push_back(DNode{});
     if (L.sph.empty()) L.sph.push_back(DSphere{});
     if (L.rect.empty()) L.rect.push_back(DRect{});
@@ -1570,6 +1699,9 @@ struct rtow_context {
     int profile = 0;  // RTOW_PROFILE=1: instrumented trace kernel, counters printed to stderr
     int lds_nodes = 1;  // simple-scene BVH staged in LDS when it fits (RTOW_LDS_NODES=0 disables; +11%, tools/ab.py)
     int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
+    // rtow_debug_trace_sample (a render with the segment-recording kernel)
+    float* dbg_out = nullptr;
+    uint32_t dbg_col = 0, dbg_row = 0, dbg_sample = 0, dbg_max = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     // scene
@@ -1604,18 +1736,18 @@ int ensure(void** p, size_t* have, size_t need) {
     return RTOW_OK;
 }
 
-template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false>
+template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const size_t lds = lds_bytes(STACK, BS, c->scene.n_node, LDSN);
     int occ = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN>, BS,
-                                                         lds));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>,
+                                                         BS, lds));
     if (occ < 1) occ = 1;
     uint32_t per = bpc ? bpc : (uint32_t)occ;
     uint32_t grid = (uint32_t)c->cus * per;
     uint32_t maxUseful = (P.n_items + BS - 1) / BS;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
-    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN>), dim3(grid), dim3(BS), lds, st, c->scene,
+    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>), dim3(grid), dim3(BS), lds, st, c->scene,
                        cam, P,
                        (uint32_t*)c->d_work, c->d_partial, (unsigned long long*)((uint8_t*)c->d_work + 8));
     HIP_TRY(hipGetLastError());
@@ -1626,6 +1758,7 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
 // c->waves picks one; 0 = the compiler's free choice
 template <int MODE, int STACK>
 int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+    if (c->dbg_out) return launchTrace<MODE, STACK, 1, false, BLOCK, false, true>(c, cam, P, bpc, st);
     if constexpr (STACK <= 32) {
         if constexpr (MODE == 0 && STACK == 16) {
             if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
@@ -1685,7 +1818,11 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     P.sky_gain = p->sky_gain;
     P.gi_gain = p->gi_gain;
     P.seed = p->seed;
-    (void)c;
+    P.dbg_out = c->dbg_out;
+    P.dbg_col = c->dbg_col;
+    P.dbg_row = c->dbg_row;
+    P.dbg_sample = c->dbg_sample;
+    P.dbg_max = c->dbg_max;
     return RTOW_OK;
 }
 
@@ -1861,6 +1998,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_refs = pushBlob(blob, L.refs), o_med = pushBlob(blob, L.med), o_mat = pushBlob(blob, L.mat);
     size_t o_tex = pushBlob(blob, L.tex), o_rv = pushBlob(blob, L.ranvec), o_perm = pushBlob(blob, L.perm);
     size_t o_img = pushBlob(blob, L.img), o_texels = pushBlob(blob, L.texels);
+    size_t o_ks = pushBlob(blob, L.sph_key), o_kr = pushBlob(blob, L.rect_key), o_km = pushBlob(blob, L.med_key);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1886,6 +2024,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.perm = (const uint32_t*)(b + o_perm);
     d.img = (const DImage*)(b + o_img);
     d.texels = (const uint8_t*)(b + o_texels);
+    d.sph_key = (const unsigned long long*)(b + o_ks);
+    d.rect_key = (const unsigned long long*)(b + o_kr);
+    d.med_key = (const unsigned long long*)(b + o_km);
     d.root = L.root;
     d.stack_need = L.stack_need;
     d.has_media = L.has_media ? 1u : 0u;
@@ -1916,6 +2057,35 @@ int rtow_render(rtow_context* c, const rtow_camera* cam, const rtow_params* p, u
     if (rc) return rc;
     if (bgra_out) HIP_TRY(hipMemcpy(bgra_out, d_bgra, npx * 4, hipMemcpyDeviceToHost));
     if (linear_out) HIP_TRY(hipMemcpy(linear_out, d_lin, npx * 12, hipMemcpyDeviceToHost));
+    return RTOW_OK;
+}
+
+int rtow_debug_trace_sample(rtow_context* c, const rtow_camera* cam, const rtow_params* p, uint32_t x, uint32_t y,
+                            uint32_t sample, float* out, uint32_t max_segments, uint32_t* n_segments) {
+    if (!c || !p || !out || max_segments == 0) return set_error(RTOW_E_INVALID, "NULL argument");
+    if (x >= p->width || y >= p->height || sample >= p->spp) return set_error(RTOW_E_INVALID, "pixel/sample out of range");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = (size_t)max_segments * RTOW_DEBUG_SEG_FLOATS * sizeof(float);
+    HIP_TRY(hipMalloc((void**)&c->dbg_out, bytes));
+    HIP_TRY(hipMemset(c->dbg_out, 0, bytes));
+    c->dbg_col = x;
+    c->dbg_row = p->height - 1 - y;
+    c->dbg_sample = sample;
+    c->dbg_max = max_segments;
+    rtow_params q = *p;
+    q.rank = 0;
+    q.world = 1;
+    rtow_stats st;
+    int rc = renderCore(c, cam, &q, nullptr, nullptr, nullptr, nullptr, c->stream, &st);
+    hipError_t e = hipSuccess;
+    if (rc == RTOW_OK) e = hipMemcpy(out, c->dbg_out, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(c->dbg_out);
+    c->dbg_out = nullptr;
+    if (rc) return rc;
+    if (e != hipSuccess) return set_error(RTOW_E_HIP, hipGetErrorString(e));
+    uint32_t n = 0;
+    while (n < max_segments && out[(size_t)n * RTOW_DEBUG_SEG_FLOATS + 11] != 0.0f) n++;
+    if (n_segments) *n_segments = n;
     return RTOW_OK;
 }
 

@@ -118,6 +118,12 @@ struct DevScene {
     const DList* list;
     const uint32_t* refs;
     const DMedium* med;
+    // Tie keys (general scenes): per sphere / rectangle / medium leaf, the
+    // order in which the reference settles an exact tie in t (see
+    // assignTieKeys in rtow_device.hip): the larger key wins.
+    const unsigned long long* sph_key;
+    const unsigned long long* rect_key;
+    const unsigned long long* med_key;
     const DMat* mat;
     const DTex* tex;
     const float* ranvec;     // 256 x float4 (xyz, pad)

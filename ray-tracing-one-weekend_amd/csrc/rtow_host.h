@@ -414,6 +414,7 @@ Hitable* randomScene_NED(World& w, SceneRng& rng, int n, const Image* earth);
 Hitable* cornellBox_NED(World& w);                 // scenes.h:355-483
 Hitable* cornellSmoke_NED(World& w);               // + smoke box of scenes.h:461-470
 Hitable* threeSphere_NED(World& w);                // config 1 (composed)
+Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth);  // config 5 (composed)
 
 // Build one of the RTOW_SCENE_* worlds the way main.cpp does (Perlin tables
 // first, then the scene, then main.cpp's root Translate when opts.wrap_world).

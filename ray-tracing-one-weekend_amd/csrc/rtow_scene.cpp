@@ -514,6 +514,61 @@ Hitable* threeSphere_NED(World& w) {
     return A.make<HitableList>(std::move(L));
 }
 
+// Config 5: book 2's final scene ("The Next Week", final chapter), which the
+// reference does not have, composed from its classes in its NED frame: NED
+// (x, y, z) = (book z, book x, -book y); the sphere cloud turns with RotateY
+// (about NED y, the reference's only rotation) where the book turns it about
+// its vertical axis.  Draws in this order: 400 box heights, then per cloud
+// sphere book x, y, z; plus one per BvhNode (oracle/ref_harness.cpp
+// finalSceneNed is the same composition over the reference's own classes).
+Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth) {
+    Arena& A = w.arena;
+    std::vector<Hitable*> L;
+    Hitable** boxes = A.list(400);
+    Hitable** cloud = A.list(1000);
+    Material* white = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.73f, 0.73f, 0.73f)));
+    Material* ground = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.48f, 0.83f, 0.53f)));
+    int b = 0;
+    for (int i = 0; i < 20; i++) {
+        for (int j = 0; j < 20; j++) {
+            float wd = 100;
+            float x0 = -1000 + i * wd;
+            float z0 = -1000 + j * wd;
+            float x1 = x0 + wd;
+            float y1 = (float)(100 * (rng() + 0.01));
+            float z1 = z0 + wd;
+            boxes[b++] = A.make<Box>(A, vec3(z0, x0, -y1), vec3(z1, x1, 0), ground);
+        }
+    }
+    L.push_back(A.make<BvhNode>(A, rng, boxes, b, 0.0f, 1.0f));
+    Material* light = A.make<DiffuseLight>(A.make<ConstantTexture>(vec3(7, 7, 7)));
+    L.push_back(A.make<XYRectangle>(147, 412, 123, 423, -554, light));
+    vec3 center(200, 400, -400);
+    L.push_back(A.make<MovingSphere>(center, center + vec3(0, 30, 0), 0.0f, 1.0f, 50.0f,
+                                     A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.7f, 0.3f, 0.1f)))));
+    L.push_back(A.make<Sphere>(vec3(45, 260, -150), 50.0f, A.make<Dielectric>(1.5f)));
+    L.push_back(A.make<Sphere>(vec3(145, 0, -150), 50.0f, A.make<Metal>(vec3(0.8f, 0.8f, 0.9f), 10.0f)));
+    Hitable* boundary = A.make<Sphere>(vec3(145, 360, -150), 70.0f, A.make<Dielectric>(1.5f));
+    L.push_back(boundary);
+    L.push_back(A.make<ConstantMedium>(A, boundary, 0.2f, A.make<ConstantTexture>(vec3(0.2f, 0.4f, 0.9f))));
+    boundary = A.make<Sphere>(vec3(0, 0, 0), 5000.0f, A.make<Dielectric>(1.5f));
+    L.push_back(A.make<ConstantMedium>(A, boundary, 0.0001f, A.make<ConstantTexture>(vec3(1.0f, 1.0f, 1.0f))));
+    Material* emat = (earth && !earth->empty())
+                         ? (Material*)A.make<Lambertian>(A.make<ImageTexture>(earth->rgb.data(), earth->nx, earth->ny))
+                         : (Material*)A.make<Dielectric>(1.5f);
+    L.push_back(A.make<Sphere>(vec3(400, 400, -200), 100.0f, emat));
+    L.push_back(A.make<Sphere>(vec3(300, 220, -280), 80.0f, A.make<Lambertian>(A.make<NoiseTexture>(true, 0.1f))));
+    for (int j = 0; j < 1000; j++) {
+        double bx = rng();
+        double by = rng();
+        double bz = rng();
+        cloud[j] = A.make<Sphere>(vec3((float)(165 * bz), (float)(165 * bx), (float)(-165 * by)), 10.0f, white);
+    }
+    L.push_back(A.make<Translate>(A.make<RotateY>(A.make<BvhNode>(A, rng, cloud, 1000, 0.0f, 1.0f), 15.0f),
+                                  vec3(395, -100, -270)));
+    return A.make<HitableList>(std::move(L));
+}
+
 static bool readRaw(const char* path, int nx, int ny, Image& im) {
     std::ifstream f(path, std::ios::binary);
     if (!f) return false;
@@ -529,13 +584,8 @@ int buildWorld(int sceneId, const rtow_build_opts& o, World& out) {
     out.perlin.generate(rng);  // static initialisation happens first (noise.h:112-116)
     Hitable* scene = nullptr;
     Arena& A = out.arena;
-    switch (sceneId) {
-    case RTOW_SCENE_THREE_SPHERE:
-        scene = threeSphere_NED(out);
-        break;
-    case RTOW_SCENE_RANDOM_NED: {
-        if (o.n < 4) return set_error(RTOW_E_INVALID, "random scene needs n >= 4");
-        const Image* earth = nullptr;
+    const Image* earth = nullptr;
+    if (sceneId == RTOW_SCENE_RANDOM_NED || sceneId == RTOW_SCENE_FINAL_NED) {
         if (o.image_mode == RTOW_IMAGE_SYNTHETIC) {
             out.images.push_back(syntheticImage(2048, 1024));
             earth = &out.images.back();
@@ -547,6 +597,13 @@ int buildWorld(int sceneId, const rtow_build_opts& o, World& out) {
             out.images.push_back(std::move(im));
             earth = &out.images.back();
         }
+    }
+    switch (sceneId) {
+    case RTOW_SCENE_THREE_SPHERE:
+        scene = threeSphere_NED(out);
+        break;
+    case RTOW_SCENE_RANDOM_NED: {
+        if (o.n < 4) return set_error(RTOW_E_INVALID, "random scene needs n >= 4");
         scene = randomScene_NED(out, rng, (int)o.n, earth);
         if (o.wrap_world) scene = A.make<Translate>(scene, vec3(0, 0, 1000));  // main.cpp:132
         break;
@@ -558,6 +615,10 @@ int buildWorld(int sceneId, const rtow_build_opts& o, World& out) {
     case RTOW_SCENE_CORNELL_SMOKE:
         scene = cornellSmoke_NED(out);
         if (o.wrap_world) scene = A.make<Translate>(scene, vec3(800, 0, 0));
+        break;
+    case RTOW_SCENE_FINAL_NED:
+        scene = finalScene_NED(out, rng, earth);
+        if (o.wrap_world) scene = A.make<Translate>(scene, vec3(600, -278, 278));
         break;
     default:
         return set_error(RTOW_E_INVALID, "unknown scene id");

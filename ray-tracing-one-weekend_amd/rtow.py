@@ -19,8 +19,9 @@ HEADER = os.path.join(REPO, "include", "rtow.h")
 # ---- constants (include/rtow.h) ---------------------------------------------
 OK, E_INVALID, E_UNSUPPORTED, E_HIP, E_NO_DEVICE, E_IO, E_NOMEM = 0, -1, -2, -3, -4, -5, -6
 SCENE_THREE_SPHERE, SCENE_RANDOM_NED, SCENE_CORNELL_NED, SCENE_CORNELL_SMOKE = 1, 2, 3, 4
+SCENE_FINAL_NED = 5
 SCENES = {"three_sphere": SCENE_THREE_SPHERE, "random_ned": SCENE_RANDOM_NED, "cornell": SCENE_CORNELL_NED,
-          "cornell_smoke": SCENE_CORNELL_SMOKE}
+          "cornell_smoke": SCENE_CORNELL_SMOKE, "final_ned": SCENE_FINAL_NED}
 IMAGE_NONE, IMAGE_SYNTHETIC, IMAGE_RAW = 0, 1, 2
 IMAGES = {"none": IMAGE_NONE, "synthetic": IMAGE_SYNTHETIC, "raw": IMAGE_RAW}
 FLAG_STATS = 1
@@ -103,6 +104,8 @@ def lib():
         "rtow_context_destroy": ([vp], i32),
         "rtow_scene_upload": ([vp, vp], i32),
         "rtow_context_set_tree": ([vp, i32], i32),
+        "rtow_debug_trace_sample": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), u32, u32, u32, vp, u32,
+                                     ctypes.POINTER(u32)], i32),
         "rtow_write_bmp": ([ctypes.c_char_p, vp, ctypes.c_uint64, u32, u32, u32], i32),
         "rtow_write_ppm": ([ctypes.c_char_p, vp, u32, u32], i32),
         "rtow_render": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)], i32),
@@ -263,6 +266,14 @@ class Context:
         check(lib().rtow_render(self._h, ctypes.byref(cam), ctypes.byref(p), bgra.ctypes.data,
                                 lin.ctypes.data if linear else None, ctypes.byref(st)), "rtow_render")
         return bgra, lin, st
+
+    def trace_sample(self, cam, p, x, y, sample, max_segments=64):
+        """rtow_debug_trace_sample: [n, 12] float32 segment records of one sample."""
+        out = np.zeros((max_segments, 12), np.float32)
+        n = ctypes.c_uint32()
+        check(lib().rtow_debug_trace_sample(self._h, ctypes.byref(cam), ctypes.byref(p), x, y, sample, out.ctypes.data,
+                                            max_segments, ctypes.byref(n)), "rtow_debug_trace_sample")
+        return out[: n.value]
 
     def render_tiles_device(self, cam, p, d_bgra_slab, d_lin_slab=None, stream=None):
         """rtow_render_tiles_device on device pointers (ints); returns Stats."""

@@ -43,6 +43,7 @@ CASES = [
     ("random487_ragged", "random_ned", 487, "synthetic", 37, 23, 8, 3),
     ("cornell", "cornell", 100, "none", 48, 48, 64, 1),
     ("cornell_smoke", "cornell_smoke", 100, "none", 48, 48, 64, 1),
+    ("final_ned", "final_ned", 100, "synthetic", 48, 48, 16, 5),
 ]
 SCENE_SEED = 1
 

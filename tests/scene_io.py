@@ -174,8 +174,25 @@ def oracle():
                                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.POINTER(OracleCounters)]
         lib.rtow_oracle_render_pixels.restype = ctypes.c_int
+        lib.rtow_oracle_trace_sample.argtypes = [ctypes.c_void_p, ctypes.POINTER(RtowCamera),
+                                                 ctypes.POINTER(RtowParams), ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_uint32)]
+        lib.rtow_oracle_trace_sample.restype = ctypes.c_int
         _oracle = lib
     return _oracle
+
+
+def oracle_trace(scene_view_ptr, cam, params, x, y, sample, max_segments=64):
+    """The oracle's path of one sample: [n, 12] float32 segment records."""
+    lib = oracle()
+    out = np.zeros((max_segments, 12), np.float32)
+    n = ctypes.c_uint32()
+    rc = lib.rtow_oracle_trace_sample(scene_view_ptr, ctypes.byref(cam), ctypes.byref(params), x, y, sample,
+                                      out.ctypes.data, max_segments, ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"oracle trace failed: {rc}")
+    return out[: n.value]
 
 
 def oracle_render(scene_view_ptr, cam, params, pixels=None, threads=None):

@@ -10,7 +10,8 @@ import torch  # noqa: E402
 torch.cuda.init()
 variants = [int(v) for v in os.environ.get("PROBE_WAVES", "0,3,4,5").split(",")]
 rounds = int(os.environ.get("PROBE_ROUNDS", "2"))
-configs = [("random_ned", 487, 1920, 1080, int(os.environ.get("PROBE_SPP", "32"))), ("cornell_smoke", 100, 800, 800, 32)]
+configs = [("random_ned", 487, 1920, 1080, int(os.environ.get("PROBE_SPP", "32"))), ("cornell_smoke", 100, 800, 800, 32),
+           ("cornell", 100, 800, 800, 32), ("final_ned", 100, 1024, 1024, 16)]
 if os.environ.get("PROBE_ONLY"):
     configs = [c for c in configs if c[0] == os.environ["PROBE_ONLY"]]
 ctxs = {}
