@@ -186,3 +186,33 @@ def test_tree_does_not_change_the_frame(scene, n):
         frames.append(ctx.render(cam, p)[1])
         ctx.close()
     assert np.array_equal(frames[0].view(np.uint32), frames[1].view(np.uint32))
+
+
+def test_long_flat_list_matches_oracle(gpu_ctx):
+    """A HitableList of 400 Boxes (final_ned's ground without its BvhNode) and
+    of all random_ned spheres: lists are walked with one continuation entry on
+    the stack, so their length is not bounded by the stack."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
+    import isolate_ground as ig
+
+    W, H, spp = 40, 24, 4
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, spp, seed=6)
+    for scene in ("final_ned", "random_ned"):
+        d = sio.scene_dict(rtow.Scene.build(scene, n=100, image="synthetic"))
+        h = d["hitables"]
+        inner = int(h[d["root"]]["a"])  # root Translate -> list (final) / BvhNode (random)
+        if h[inner]["kind"] == 9:
+            bvh = int(d["refs"][int(h[inner]["a"])])
+            e, L = ig.add_list(d, ig.leaves(h, bvh))
+            e = ig.with_items(e, inner, [L])
+        else:
+            e, L = ig.add_list(d, ig.leaves(h, inner))
+            e["hitables"][e["root"]]["a"] = L
+        sc = sio.ArrayScene(e)
+        gpu_ctx.upload(sc)
+        _, lin, _ = gpu_ctx.render(cam, p)
+        olin, _, _ = sio.oracle_render(sc.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                       sio.RtowParams.from_buffer_copy(bytes(p)))
+        assert (channel_rms(lin, olin) <= RMS_TOL).all(), scene
