@@ -32,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -46,7 +47,7 @@ using namespace rtow_dev;
 namespace {
 
 constexpr int BLOCK = 256;
-constexpr int MAXCHAIN = 4;
+constexpr int ROOTCHAIN = 4;  // DevScene::root_chain (simple scenes)
 
 // ---------------------------------------------------------------------------
 // small vector math with the reference's exact operation order (vec3.h)
@@ -127,37 +128,55 @@ __device__ __forceinline__ Ray apply_inst(const DevScene& S, uint32_t ref, const
     return q;
 }
 
-__device__ __forceinline__ Ray chain_ray(const DevScene& S, const uint32_t* ch, int n, const Ray& w) {
+// the ray through a simple scene's root instances (registers, kernel argument)
+__device__ __forceinline__ Ray root_ray(const DevScene& S, const Ray& w) {
     Ray r = w;
 #pragma unroll
-    for (int k = 0; k < MAXCHAIN; k++)
-        if (k < n) r = apply_inst(S, ch[k], r);
+    for (int k = 0; k < ROOTCHAIN; k++)
+        if (k < (int)S.root_chain_n) r = apply_inst(S, S.root_chain[k], r);
     return r;
 }
 
-// the way out of the instances, innermost first (hitable.h:28-36, 53-62, 137-150)
-__device__ __forceinline__ void chain_out(const DevScene& S, const uint32_t* ch, int n, F3& p, F3& nrm) {
+// the ray in the frame of chain `id` (DevScene::chains), outermost first
+__device__ __forceinline__ Ray chain_ray(const DevScene& S, uint32_t id, const Ray& w) {
+    const DChain& C = S.chains[id];
+    const int n = (int)C.n;
+    Ray r = w;
+    for (int k = 0; k < n; k++) r = apply_inst(S, C.ref[k], r);
+    return r;
+}
+
+// the way out of one instance (hitable.h:28-36, 53-62, 137-150)
+__device__ __forceinline__ void inst_out(const DevScene& S, uint32_t ref, F3& p, F3& nrm);
+
+// the way out of the instances, innermost first
+__device__ __forceinline__ void chain_out(const DevScene& S, uint32_t id, F3& p, F3& nrm) {
+    const DChain& C = S.chains[id];
+    for (int k = (int)C.n - 1; k >= 0; k--) inst_out(S, C.ref[k], p, nrm);
+}
+
+__device__ __forceinline__ void root_out(const DevScene& S, F3& p, F3& nrm) {
 #pragma unroll
-    for (int k = MAXCHAIN - 1; k >= 0; k--) {
-        if (k < n) {
-            const uint32_t ref = ch[k];
-            const uint32_t ik = ref >> KIND_SHIFT;
-            const DInst& I = S.inst[ref & INDEX_MASK];
-            if (ik == DK_FLIP) {
-                nrm = neg(nrm);
-            } else if (ik == DK_TRANSLATE) {
-                p = add(p, f3(I.p[0], I.p[1], I.p[2]));
-            } else {
-                const float s = I.p[0], c = I.p[1];
-                F3 q = p, m = nrm;
-                q.x = c * p.x + s * p.z;
-                q.z = -s * p.x + c * p.z;
-                m.x = c * nrm.x + s * nrm.z;
-                m.z = -s * nrm.x + c * nrm.z;
-                p = q;
-                nrm = m;
-            }
-        }
+    for (int k = ROOTCHAIN - 1; k >= 0; k--)
+        if (k < (int)S.root_chain_n) inst_out(S, S.root_chain[k], p, nrm);
+}
+
+__device__ __forceinline__ void inst_out(const DevScene& S, uint32_t ref, F3& p, F3& nrm) {
+    const uint32_t ik = ref >> KIND_SHIFT;
+    const DInst& I = S.inst[ref & INDEX_MASK];
+    if (ik == DK_FLIP) {
+        nrm = neg(nrm);
+    } else if (ik == DK_TRANSLATE) {
+        p = add(p, f3(I.p[0], I.p[1], I.p[2]));
+    } else {
+        const float s = I.p[0], c = I.p[1];
+        F3 q = p, m = nrm;
+        q.x = c * p.x + s * p.z;
+        q.z = -s * p.x + c * p.z;
+        m.x = c * nrm.x + s * nrm.z;
+        m.z = -s * nrm.x + c * nrm.z;
+        p = q;
+        nrm = m;
     }
 }
 
@@ -286,7 +305,7 @@ __device__ __forceinline__ void rect_axes(uint32_t axis, uint32_t& i, uint32_t& 
 }
 __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, float t1, float& t) {
     uint32_t i, j, k;
-    rect_axes(q.axis, i, j, k);
+    rect_axes(q.axis & 3u, i, j, k);
     const float tt = (q.k - comp(r.o, k)) / comp(r.d, k);
     if (tt < t0 || tt > t1) return false;
     const float x = comp(r.o, i) + tt * comp(r.d, i);
@@ -463,34 +482,44 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
 
 struct Best {
     float t;
-    uint32_t prim;
-    uint32_t ch[MAXCHAIN];
-    int n;
+    uint32_t prim;  // the leaf; its instance chain is the leaf's own (DSphere::chain ...)
 };
 
-__device__ __forceinline__ void chain_push(uint32_t* ch, int& n, uint32_t ref) {
-#pragma unroll
-    for (int k = 0; k < MAXCHAIN; k++)
-        if (k == n) ch[k] = ref;
-    n++;
-}
-
-__device__ __forceinline__ void take_best(Best& b, uint32_t prim, const uint32_t* ch, int n) {
-    b.prim = prim;
-#pragma unroll
-    for (int k = 0; k < MAXCHAIN; k++) b.ch[k] = ch[k];
-    b.n = n;
+// ConstantMedium's two boundary queries (constantMedium.h:28-29) when the
+// boundary is a plain sphere: hit(-FLT_MAX, FLT_MAX) takes the near root,
+// hit(t1 + 0.0001, FLT_MAX) then rejects the near root again and takes the
+// far one -- the same roots Sphere::hit (sphere.h:20-69) computes each call.
+template <bool UNIT_TIME>
+__device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, float a, float& t1, float& t2) {
+    const F3 oc = sub(r.o, sph_center<UNIT_TIME>(s, r.time));
+    const float b = dot(r.d, oc);
+    const float c = dot(oc, oc) - s.r * s.r;
+    const float disc = b * b - a * c;
+    if (!(disc > 0)) return false;
+    const float sq = sqrtf(disc);
+    const float tn = (-b - sq) / a, tf = (-b + sq) / a;
+    const float lo = -FLT_MAX;
+    float first;
+    if (tn < FLT_MAX && tn > lo) first = tn;
+    else if (tf < FLT_MAX && tf > lo) first = tf;
+    else return false;
+    const float lo2 = (float)((double)first + 0.0001);
+    if (tn < FLT_MAX && tn > lo2) t2 = tn;
+    else if (tf < FLT_MAX && tf > lo2) t2 = tf;
+    else return false;
+    t1 = first;
+    return true;
 }
 
 // Closest hit of `root` for a world-space ray, reference semantics, any scene
 // graph: lists in order with a shrinking tmax (hitableList.h:20-38),
-// instances, rectangles, media.  stk: this lane's LDS stack column.
+// instances, rectangles, media; exact ties settled by the tie keys.
+// `r` is the ray in the frame of chain `chain0` (the frame `root` sits in).
+// stk: this lane's LDS stack column.
 template <bool MEDIA, int STACK>
-__device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, float tmin, float tmax, uint32_t* stk,
-                         int sp0, Rng& rng, Best& best, uint32_t& overflow) {
-    uint32_t ch[MAXCHAIN] = {0, 0, 0, 0};
-    int cn = 0;
-    Ray r = wray;
+__device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
+                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow) {
+    Ray r = chain_ray(S, chain0, wray);
     SlabRay q = slab_ray(r);
     float a = dot(r.d, r.d);
     float bt = tmax;
@@ -507,7 +536,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
                                      ? bvh_step<true, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow)
                                      : bvh_step<false, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow);
             if (b != before) {
-                take_best(best, b, ch, cn);
+                best.prim = b;
                 found = true;
             }
             if ((nxt >> KIND_SHIFT) != DK_NONE) {
@@ -521,7 +550,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
             if (sph_root(c, s.r, r, a, tmin, t) &&
                 (t < bt || (t == bt && wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0))))) {
                 bt = t;
-                take_best(best, cur, ch, cn);
+                best.prim = cur;
                 found = true;
             }
         } else if (kind == DK_RECT) {
@@ -529,38 +558,41 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
             if (rect_t(S.rect[idx], r, tmin, bt, t) &&
                 (t < bt || wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0)))) {
                 bt = t;
-                take_best(best, cur, ch, cn);
+                best.prim = cur;
                 found = true;
             }
-        } else if (kind == DK_LIST) {
-            const DList L = S.list[idx];
-            if (L.count > 0) {
-                for (uint32_t k = L.count - 1; k >= 1; k--) {
+        } else if (kind == DK_LIST || kind == DK_LISTNEXT) {
+            // items in order; one continuation entry below the item being
+            // visited instead of the whole rest of the list
+            const uint32_t at = kind == DK_LIST ? S.list[idx].first : idx;
+            const uint32_t item = S.refs[at];
+            if ((item >> KIND_SHIFT) != DK_NONE) {
+                if ((S.refs[at + 1] >> KIND_SHIFT) != DK_NONE) {
                     if (sp < STACK) {
-                        stk[sp * BLOCK] = S.refs[L.first + k];
+                        stk[sp * BLOCK] = mkref(DK_LISTNEXT, at + 1);
                         sp++;
                     } else {
                         overflow = 1;
                     }
                 }
-                cur = S.refs[L.first];
+                cur = item;
                 continue;
             }
         } else if (kind == DK_TRANSLATE || kind == DK_ROTY || kind == DK_FLIP) {
-            if (sp < STACK && cn < MAXCHAIN) {
-                stk[sp * BLOCK] = mkref(DK_EXIT, 0);
+            // enter: the EXIT marker remembers the chain to restore
+            const DInst& I = S.inst[idx];
+            if (sp < STACK) {
+                stk[sp * BLOCK] = mkref(DK_EXIT, I.parent_chain);
                 sp++;
-                chain_push(ch, cn, cur);
                 r = apply_inst(S, cur, r);
                 q = slab_ray(r);
                 a = dot(r.d, r.d);
-                cur = S.inst[idx].child;
+                cur = I.child;
                 continue;
             }
             overflow = 1;
         } else if (kind == DK_EXIT) {
-            cn--;
-            r = chain_ray(S, ch, cn, wray);
+            r = chain_ray(S, idx, wray);
             q = slab_ray(r);
             a = dot(r.d, r.d);
         } else if (kind == DK_MEDIUM) {
@@ -569,24 +601,33 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, floa
                 // hit as tmax (hitableList.h:30)
                 const DMedium M = S.med[idx];
                 (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
-                Best b1, b2;
-                if (traverse<false, STACK>(S, M.boundary, r, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow)) {
-                    const float t1 = b1.t;
-                    if (traverse<false, STACK>(S, M.boundary, r, (float)((double)t1 + 0.0001), FLT_MAX, stk, sp, rng,
-                                               b2, overflow)) {
-                        float ta = t1, tb = b2.t;
-                        if (ta < tmin) ta = tmin;
-                        if (tb > bt) tb = bt;
-                        if (!(ta >= tb)) {
-                            if (ta < 0) ta = 0;
-                            const float dl = len(r.d);
-                            const float inside = (tb - ta) * dl;
-                            const float dist = (float)(-(1 / M.density) * log(rng.next()));
-                            if (dist < inside) {
-                                bt = ta + dist / dl;
-                                take_best(best, cur, ch, cn);
-                                found = true;
-                            }
+                float t1 = 0, t2 = 0;
+                bool two;
+                if ((M.boundary >> KIND_SHIFT) == DK_SPHERE) {
+                    const Sph s = load_sph(S.sph + (M.boundary & INDEX_MASK));
+                    two = S.unit_time ? sphere_boundary<true>(s, r, a, t1, t2) : sphere_boundary<false>(s, r, a, t1, t2);
+                } else {
+                    Best b1, b2;
+                    two = traverse<false, STACK>(S, M.boundary, wray, M.chain, -FLT_MAX, FLT_MAX, stk, sp, rng, b1,
+                                                 overflow) &&
+                          traverse<false, STACK>(S, M.boundary, wray, M.chain, (float)((double)b1.t + 0.0001), FLT_MAX,
+                                                 stk, sp, rng, b2, overflow);
+                    t1 = b1.t;
+                    t2 = b2.t;
+                }
+                if (two) {
+                    float ta = t1, tb = t2;
+                    if (ta < tmin) ta = tmin;
+                    if (tb > bt) tb = bt;
+                    if (!(ta >= tb)) {
+                        if (ta < 0) ta = 0;
+                        const float dl = len(r.d);
+                        const float inside = (tb - ta) * dl;
+                        const float dist = (float)(-(1 / M.density) * log(rng.next()));
+                        if (dist < inside) {
+                            bt = ta + dist / dl;
+                            best.prim = cur;
+                            found = true;
                         }
                     }
                 }
@@ -608,13 +649,16 @@ __device__ __forceinline__ void sphere_uv(F3 p, float& u, float& v) {
     v = (float)((theta + M_PI / 2) / M_PI);
 }
 
-// The HitRecord of the winning primitive: local ray through the chain, the
-// primitive's record, then the instances' way out.
-__device__ void finalize(const DevScene& S, uint32_t prim, float t, const uint32_t* ch, int cn, const Ray& wray,
-                         Rec& rec) {
-    const Ray r = chain_ray(S, ch, cn, wray);
+// The HitRecord of the winning leaf: the ray into the leaf's frame (its
+// instance chain), the leaf's record, then the instances' way out.
+// SIMPLE: every leaf sits under the root chain (kernel-argument registers).
+template <bool SIMPLE>
+__device__ void finalize(const DevScene& S, uint32_t prim, float t, const Ray& wray, Rec& rec) {
     const uint32_t kind = prim >> KIND_SHIFT;
     const uint32_t idx = prim & INDEX_MASK;
+    const uint32_t chain =
+        SIMPLE ? 0u : (kind == DK_SPHERE ? S.sph[idx].chain : (kind == DK_RECT ? S.rect[idx].chain : S.med[idx].chain));
+    const Ray r = SIMPLE ? root_ray(S, wray) : chain_ray(S, chain, wray);
     rec.t = t;
     rec.u = 0.0f;
     rec.v = 0.0f;
@@ -627,13 +671,15 @@ __device__ void finalize(const DevScene& S, uint32_t prim, float t, const uint32
     } else if (kind == DK_RECT) {
         const DRect& q = S.rect[idx];
         uint32_t i, j, k;
-        rect_axes(q.axis, i, j, k);
+        rect_axes(q.axis & 3u, i, j, k);
         const float x = comp(r.o, i) + t * comp(r.d, i);
         const float y = comp(r.o, j) + t * comp(r.d, j);
         rec.u = (x - q.a0) / (q.a1 - q.a0);
         rec.v = (y - q.b0) / (q.b1 - q.b0);
         rec.p = at(r, t);
-        rec.n = f3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
+        const float nv = (q.axis & RECT_FLIP) ? -1.0f : 1.0f;  // FlipNormals folded into the leaf
+        const float zero = (q.axis & RECT_FLIP) ? -0.0f : 0.0f;
+        rec.n = f3(k == 0 ? nv : zero, k == 1 ? nv : zero, k == 2 ? nv : zero);
         rec.mat = q.mat;
     } else {  // DK_MEDIUM
         const DMedium& m = S.med[idx];
@@ -641,7 +687,10 @@ __device__ void finalize(const DevScene& S, uint32_t prim, float t, const uint32
         rec.n = f3(1, 0, 0);
         rec.mat = m.phase_mat;
     }
-    chain_out(S, ch, cn, rec.p, rec.n);
+    if (SIMPLE)
+        root_out(S, rec.p, rec.n);
+    else
+        chain_out(S, chain, rec.p, rec.n);
 }
 
 // ---------------------------------------------------------------------------
@@ -928,7 +977,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 prof.cyc_other += t_now - t_mark;
                 t_mark = t_now;
             }
-            const Ray lray = chain_ray(S, S.root_chain, (int)S.root_chain_n, ray);
+            const Ray lray = root_ray(S, ray);
             float bt = FLT_MAX;
             const uint32_t prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
             hit = (prim >> KIND_SHIFT) != DK_NONE;
@@ -937,13 +986,12 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 prof.cyc_trav += t_now - t_mark;
                 t_mark = t_now;
             }
-            if (hit) finalize(S, prim, bt, S.root_chain, (int)S.root_chain_n, ray, rec);
+            if (hit) finalize<true>(S, prim, bt, ray, rec);
         } else {
             Best best;
             best.prim = 0;
-            best.n = 0;
-            hit = traverse<MODE == 3, STACK>(S, S.root, ray, 0.001f, FLT_MAX, stk, 0, rng, best, overflow);
-            if (hit) finalize(S, best.prim, best.t, best.ch, best.n, ray, rec);
+            hit = traverse<MODE == 3, STACK>(S, S.root, ray, 0u, 0.001f, FLT_MAX, stk, 0, rng, best, overflow);
+            if (hit) finalize<false>(S, best.prim, best.t, ray, rec);
         }
         if constexpr (DBG) {
             if (col == P.dbg_col && row == P.dbg_row && s == P.dbg_sample) {
@@ -1128,6 +1176,7 @@ struct HostLayout {
     uint32_t root_chain[4] = {0, 0, 0, 0};
     uint32_t bvh_root = 0;
     std::vector<unsigned long long> sph_key, rect_key, med_key;
+    std::vector<DChain> chains;
 };
 
 // ---------------------------------------------------------------------------
@@ -1145,6 +1194,87 @@ struct HostLayout {
 // boundary are queried for t alone and get no key.  (Not reproduced: a
 // BvhNode ITEM of a list whose box the ray enters exactly at the tied t is
 // culled by AABB::hit's `tmax <= tmin`, so its leaf cannot take the tie.)
+// Instance chains: every leaf / medium / instance gets the id (in L.chains)
+// of the chain of instances above it; EXIT markers restore an instance's
+// parent chain.  A node met again under a different chain (an instance
+// shared between two transforms) is rejected.
+struct ChainAssigner {
+    HostLayout& L;
+    std::map<std::vector<uint32_t>, uint32_t> ids;
+    std::vector<uint32_t> cur;
+    std::vector<uint32_t> sph, rect, med, inst;  // assigned chain per entity (~0u: not yet)
+    std::string err;
+
+    explicit ChainAssigner(HostLayout& l) : L(l) {
+        sph.assign(L.sph.size(), ~0u);
+        rect.assign(L.rect.size(), ~0u);
+        med.assign(L.med.size(), ~0u);
+        inst.assign(L.inst.size(), ~0u);
+        id();  // chain 0: no instances
+    }
+    uint32_t id() {
+        auto it = ids.find(cur);
+        if (it != ids.end()) return it->second;
+        DChain c{};
+        c.n = (uint32_t)cur.size();
+        for (size_t k = 0; k < cur.size() && k < (size_t)MAXCHAIN; k++) c.ref[k] = cur[k];
+        L.chains.push_back(c);
+        return ids[cur] = (uint32_t)L.chains.size() - 1;
+    }
+    bool set(std::vector<uint32_t>& v, uint32_t i, uint32_t c) {
+        if (v[i] != ~0u && v[i] != c) {
+            err = "a hitable is shared under two different instance chains";
+            return false;
+        }
+        v[i] = c;
+        return true;
+    }
+    void walk(uint32_t ref, int depth = 0) {
+        if (!err.empty() || depth > 4096) return;
+        const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+        if (cur.size() > (size_t)MAXCHAIN) {
+            err = "instance nesting deeper than " + std::to_string(MAXCHAIN);
+            return;
+        }
+        const uint32_t c = id();
+        switch (kind) {
+        case DK_SPHERE:
+            if (set(sph, idx, c)) L.sph[idx].chain = c;
+            break;
+        case DK_RECT:
+            if (set(rect, idx, c)) L.rect[idx].chain = c;
+            break;
+        case DK_MEDIUM:
+            if (set(med, idx, c)) {
+                L.med[idx].chain = c;
+                walk(L.med[idx].boundary, depth + 1);
+            }
+            break;
+        case DK_BVH:
+            walk(L.bvh[idx].left, depth + 1);
+            walk(L.bvh[idx].right, depth + 1);
+            break;
+        case DK_LIST: {
+            const DList l = L.list[idx];
+            for (uint32_t j = 0; j < l.count; j++) walk(L.refs[l.first + j], depth + 1);
+            break;
+        }
+        case DK_TRANSLATE:
+        case DK_ROTY:
+        case DK_FLIP:
+            if (set(inst, idx, c)) {
+                L.inst[idx].parent_chain = c;
+                cur.push_back(ref);
+                walk(L.inst[idx].child, depth + 1);
+                cur.pop_back();
+            }
+            break;
+        default:
+            break;
+        }
+    }
+};
+
 struct KeyComp {
     uint32_t bits;
     unsigned long long closed, open;
@@ -1370,6 +1500,12 @@ struct Converter {
                 mx[a] = h.f[a] + h.f[3];
             }
             return true;
+        case RTOW_HIT_BOX:  // box.h:16-19: every side lies on it
+            for (int a = 0; a < 3; a++) {
+                mn[a] = h.f[a];
+                mx[a] = h.f[3 + a];
+            }
+            return true;
         case RTOW_HIT_MOVING_SPHERE: {
             const float r = h.f[8];
             for (int a = 0; a < 3; a++) {
@@ -1433,6 +1569,17 @@ struct Converter {
             break;
         }
         case RTOW_HIT_FLIP_NORMALS:
+            if (s.hitables[h.a].kind >= RTOW_HIT_RECT_XY && s.hitables[h.a].kind <= RTOW_HIT_RECT_YZ) {
+                // FlipNormals(rectangle): the flip folds into a copy of the leaf
+                const uint32_t leaf = conv(h.a, underBvh);
+                if ((leaf >> KIND_SHIFT) != DK_RECT) return mkref(DK_NONE, 0);
+                DRect d = L.rect[leaf & INDEX_MASK];
+                d.axis ^= RECT_FLIP;
+                ref = mkref(DK_RECT, (uint32_t)L.rect.size());
+                L.rect.push_back(d);
+                break;
+            }
+            [[fallthrough]];
         case RTOW_HIT_TRANSLATE:
         case RTOW_HIT_ROTATE_Y: {
             uint32_t k = h.kind == RTOW_HIT_FLIP_NORMALS ? DK_FLIP : (h.kind == RTOW_HIT_TRANSLATE ? DK_TRANSLATE : DK_ROTY);
@@ -1453,7 +1600,8 @@ struct Converter {
             ref = mkref(DK_LIST, slot);
             memo[hi] = ref;
             uint32_t first = (uint32_t)L.refs.size();
-            L.refs.resize(L.refs.size() + h.b);
+            L.refs.resize(L.refs.size() + h.b + 1);
+            L.refs[first + h.b] = mkref(DK_NONE, 0);  // end of this list's items (DK_LISTNEXT)
             for (uint32_t i = 0; i < h.b; i++) {
                 uint32_t c = conv(s.refs[h.a + i], underBvh);
                 L.refs[first + i] = c;
@@ -1532,7 +1680,7 @@ struct Bounds {
             const DList& l = L.list[idx];
             for (uint32_t i = 0; i < l.count; i++) {
                 auto c = need(L.refs[l.first + i], inMedium);
-                r.first = std::max(r.first, (l.count - 1 - i) + c.first);
+                r.first = std::max(r.first, (i + 1 < l.count ? 1u : 0u) + c.first);  // one DK_LISTNEXT
                 r.second = std::max(r.second, c.second);
             }
             break;
@@ -1595,7 +1743,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     {
         uint32_t r = L.root;
         uint32_t n = 0;
-        while (n < (uint32_t)MAXCHAIN) {
+        while (n < (uint32_t)ROOTCHAIN) {
             const uint32_t k = r >> KIND_SHIFT;
             if (k != DK_TRANSLATE && k != DK_ROTY && k != DK_FLIP) break;
             L.root_chain[n++] = r;
@@ -1668,6 +1816,11 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     if (s.n_texel_bytes) L.texels.assign(s.texels, s.texels + s.n_texel_bytes);
     // keep every array non-empty so each gets a valid device pointer
     if (L.bvh.empty()) L.bvh.push_back(DBvh{});
+    {
+        ChainAssigner ca(L);
+        ca.walk(L.root);
+        if (!ca.err.empty()) return set_error(RTOW_E_UNSUPPORTED, ca.err);
+    }
     L.sph_key.assign(L.sph.size(), 0ull);
     L.rect_key.assign(L.rect.size(), 0ull);
     L.med_key.assign(L.med.size(), 0ull);
@@ -1998,6 +2151,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_refs = pushBlob(blob, L.refs), o_med = pushBlob(blob, L.med), o_mat = pushBlob(blob, L.mat);
     size_t o_tex = pushBlob(blob, L.tex), o_rv = pushBlob(blob, L.ranvec), o_perm = pushBlob(blob, L.perm);
     size_t o_img = pushBlob(blob, L.img), o_texels = pushBlob(blob, L.texels);
+    size_t o_ch = pushBlob(blob, L.chains);
     size_t o_ks = pushBlob(blob, L.sph_key), o_kr = pushBlob(blob, L.rect_key), o_km = pushBlob(blob, L.med_key);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
@@ -2024,6 +2178,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.perm = (const uint32_t*)(b + o_perm);
     d.img = (const DImage*)(b + o_img);
     d.texels = (const uint8_t*)(b + o_texels);
+    d.chains = (const DChain*)(b + o_ch);
     d.sph_key = (const unsigned long long*)(b + o_ks);
     d.rect_key = (const unsigned long long*)(b + o_kr);
     d.med_key = (const unsigned long long*)(b + o_km);

@@ -31,6 +31,7 @@ enum : uint32_t {
     DK_FLIP = 7,
     DK_MEDIUM = 8,
     DK_EXIT = 9,  // traversal-stack marker: leave the innermost instance
+    DK_LISTNEXT = 10,  // traversal-stack marker: continue a list at refs[index]
     DK_NONE = 15
 };
 
@@ -64,22 +65,39 @@ struct alignas(16) DNode {
 // u,v (sphere.h:93-118 never writes them).
 // dc = center1 - center0 is computed once on the host: the same float
 // subtraction center() performs on every call (sphere.h:130).
+// Leaves carry `chain`: the index in DevScene::chains of the instance chain
+// (root first) their path from the root passes through, so a hit record needs
+// only the leaf to be carried out of its instances.  (Every node is reached
+// on one path: rtow_scene_upload rejects an instance shared under two
+// different chains.)
 struct alignas(16) DSphere {  // 48 B
     float c0[3], r;
     float dc[3], t0;
     float t1;
-    uint32_t mat, moving, pad;
+    uint32_t mat, moving, chain;
 };
 
-struct alignas(16) DRect {  // 32 B, xy_rect.h; axis: 0 XY (k on z), 1 XZ (k on y), 2 YZ (k on x)
+// xy_rect.h; axis & 3: 0 XY (k on z), 1 XZ (k on y), 2 YZ (k on x).
+// axis & RECT_FLIP: a FlipNormals directly above the rectangle (hitable.h:28-36)
+// folded into the leaf.
+constexpr uint32_t RECT_FLIP = 4u;
+struct alignas(16) DRect {  // 32 B
     float a0, a1, b0, b1;
     float k;
-    uint32_t axis, mat, pad;
+    uint32_t axis, mat, chain;
 };
 
-struct alignas(16) DInst {  // 32 B: TRANSLATE p = offset; ROTY p[0] sin, p[1] cos; FLIP -
-    uint32_t child, pad;
+// TRANSLATE p = offset; ROTY p[0] sin, p[1] cos; FLIP -.  parent_chain: the
+// chain in force where the instance sits (restored when the traversal leaves it).
+struct alignas(16) DInst {  // 32 B
+    uint32_t child, parent_chain;
     float p[6];
+};
+
+constexpr int MAXCHAIN = 7;
+struct alignas(16) DChain {  // 32 B: instance refs, outermost first
+    uint32_t n;
+    uint32_t ref[MAXCHAIN];
 };
 
 struct alignas(16) DList {  // 16 B: children at refs[first .. first+count)
@@ -89,7 +107,7 @@ struct alignas(16) DList {  // 16 B: children at refs[first .. first+count)
 struct alignas(16) DMedium {  // 16 B, constantMedium.h:21-23
     uint32_t boundary, phase_mat;
     float density;
-    uint32_t pad;
+    uint32_t chain;
 };
 
 struct alignas(16) DMat {  // 32 B
@@ -118,6 +136,7 @@ struct DevScene {
     const DList* list;
     const uint32_t* refs;
     const DMedium* med;
+    const DChain* chains;
     // Tie keys (general scenes): per sphere / rectangle / medium leaf, the
     // order in which the reference settles an exact tie in t (see
     // assignTieKeys in rtow_device.hip): the larger key wins.
