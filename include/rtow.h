@@ -248,6 +248,12 @@ uint32_t rtow_scene_draws(const rtow_scene_buf* buf);
 
 /* The camera main.cpp:111-125 constructs for a width x height frame. */
 int rtow_camera_main(uint32_t width, uint32_t height, rtow_camera* out);
+/* The main camera after the GUI frame loop moved it (main.cpp:476/554 and
+ * 624-628): Camera::setOrientationMatrix with rows view (w), east (u), down
+ * (v) -- rows[0..2], [3..5], [6..8] -- and Camera::setLookFromPoint; the basis
+ * as setCamera_QuaternionMatrix (camera.h:315-342) forms it. */
+int rtow_camera_oriented(uint32_t width, uint32_t height, const float look_from[3], const float rows[9],
+                         rtow_camera* out);
 /* Fill an RGB8 image with the synthetic "earth" stand-in. */
 void rtow_synthetic_image(uint32_t nx, uint32_t ny, uint8_t* rgb);
 
@@ -298,6 +304,20 @@ int rtow_context_set_tree(rtow_context* ctx, int tree);
  * Synchronous. */
 int rtow_render(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
                 uint8_t* bgra_out, float* linear_out, rtow_stats* stats);
+
+/* Progressive rendering: the reference's GUI frame loop re-renders the frame
+ * every iteration (main.cpp:247-687, camera updated through
+ * setOrientationMatrix camera.h:231-235 / setLookFromPoint); here each call
+ * renders p->spp NEW samples per pixel -- sample indices continue after the
+ * ones already accumulated, so the random streams never repeat -- adds them to
+ * the context's running sums and writes the average of everything so far.
+ * The sums restart when `reset` is set or the camera or any parameter other
+ * than spp / samples_per_chunk / blocks_per_cu / flags changed.  total_spp
+ * (may be NULL) receives the samples per pixel accumulated.  F frames of S
+ * spp give the frame of one rtow_render of F*S spp with samples_per_chunk = S,
+ * bit for bit. */
+int rtow_render_progressive(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p, int reset,
+                            uint8_t* bgra_out, float* linear_out, uint32_t* total_spp, rtow_stats* stats);
 
 /* Render this rank's tiles (p->rank of p->world) into compact DEVICE slabs:
  * tile-slot s of the rank holds global tile rank + s*world, 64 pixels row-major

@@ -20,6 +20,7 @@
 // Usage:
 //   ref_harness dump   <scene> <out.scn> [opts]
 //   ref_harness camera <W> <H> <out.cam>
+//   ref_harness camera_oriented <W> <H> <lookfrom xyz> <view xyz> <east xyz> <down xyz> <out.cam>
 //   ref_harness render <scene> <W> <H> <spp> <out_prefix> [opts]
 //       writes <out_prefix>.lin (W*H*3 float32, framebuffer order) and
 //       <out_prefix>.bgra (W*H*4 bytes, main.cpp:982-989)
@@ -542,6 +543,22 @@ int main(int argc, char** argv) {
     if (cmd == "camera" && argc >= 5) {
         Camera* c = mainCamera((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]));
         writeCamera(argv[4], c);
+        return 0;
+    }
+    if (cmd == "camera_oriented" && argc >= 17) {
+        // the main camera after the frame loop's updates (main.cpp:476/554,
+        // 624-628): setOrientationMatrix(rows view/east/down) + setLookFromPoint
+        Camera* c = mainCamera((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]));
+        float v[12];
+        for (int k = 0; k < 12; k++) v[k] = (float)std::atof(argv[4 + k]);
+        mat4x4 m;
+        m.m[0] = vec4(v[3], v[4], v[5], 0.0f);
+        m.m[1] = vec4(v[6], v[7], v[8], 0.0f);
+        m.m[2] = vec4(v[9], v[10], v[11], 0.0f);
+        m.m[3] = vec4(0.0f, 0.0f, 0.0f, 1.0f);
+        c->setOrientationMatrix(m);
+        c->setLookFromPoint(vec3(v[0], v[1], v[2]));
+        writeCamera(argv[16], c);
         return 0;
     }
     if (cmd == "render" && argc >= 7) {

@@ -98,6 +98,7 @@ struct DevParams {
     float sky_gain, gi_gain;
     uint64_t seed;
     uint32_t n_items;
+    uint32_t sample_base;  // progressive frames: the samples already accumulated (RNG sample index offset)
     // rtow_debug_trace_sample: the one (column, row, sample) whose segments
     // the DBG kernel records (RTOW_DEBUG_SEG_FLOATS floats each) into dbg_out
     uint32_t dbg_col, dbg_row, dbg_sample, dbg_max;
@@ -948,7 +949,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         }
         if (need_sample) {
             // main.cpp:943-946 + camera.h:123-135 (CAMERA_DOF_EN 0)
-            rng.key = rtow_sample_key(P.seed, row * P.width + col, s);
+            rng.key = rtow_sample_key(P.seed, row * P.width + col, P.sample_base + s);
             rng.ctr = 0;
             const float u = (float)((double)col + rng.next()) / (float)P.width;
             const float v = (float)((double)row + rng.next()) / (float)P.height;
@@ -1079,8 +1080,11 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     }
 }
 
+// accum (progressive frames, single rank): running per-pixel sums of all
+// frames; this frame's chunk sums are added to it in order, and the average
+// is over P.sample_base + P.spp samples.
 __global__ void resolve_kernel(DevParams P, const float4* partial, uint8_t* slab_bgra, float* slab_lin,
-                               uint8_t* fb_bgra, float* fb_lin) {
+                               uint8_t* fb_bgra, float* fb_lin, float4* accum) {
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= P.n_local_px) return;
     uint32_t x, yimg;
@@ -1100,7 +1104,14 @@ __global__ void resolve_kernel(DevParams P, const float4* partial, uint8_t* slab
         const float4 b = partial[(size_t)c * P.n_local_px + lp];
         acc = add(acc, f3(b.x, b.y, b.z));
     }
-    const float k = (float)(1.0 / (double)(float)P.spp);  // vec3.h:133-139
+    if (accum) {
+        if (P.sample_base) {
+            const float4 prev = accum[lp];
+            acc = add(f3(prev.x, prev.y, prev.z), acc);
+        }
+        accum[lp] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+    }
+    const float k = (float)(1.0 / (double)(float)(P.sample_base + P.spp));  // vec3.h:133-139
     const F3 lin = f3(acc.x * k, acc.y * k, acc.z * k);
     const float sq[3] = {sqrtf(lin.x), sqrtf(lin.y), sqrtf(lin.z)};
     uint32_t q[3];
@@ -1867,6 +1878,11 @@ struct rtow_context {
     size_t partial_bytes = 0;
     uint8_t* d_fb = nullptr;  // rtow_render: BGRA frame + linear frame
     size_t fb_bytes = 0;
+    // rtow_render_progressive: running sums, samples so far, what they were rendered with
+    float4* d_accum = nullptr;
+    size_t accum_bytes = 0;
+    uint32_t accum_spp = 0;
+    std::vector<uint8_t> accum_sig;
 };
 
 namespace {
@@ -1922,6 +1938,7 @@ int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
         if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
         if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
         if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
+        if (c->waves == 2) return launchTrace<MODE, STACK, 2>(c, cam, P, bpc, st);
     }
     return launchTrace<MODE, STACK, 1>(c, cam, P, bpc, st);
 }
@@ -1997,13 +2014,15 @@ DevCam makeCam(const rtow_camera* cam) {
 
 // trace + resolve on `st`; outputs may be NULL
 int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, uint8_t* slab_bgra, float* slab_lin,
-               uint8_t* fb_bgra, float* fb_lin, hipStream_t st, rtow_stats* stats) {
+               uint8_t* fb_bgra, float* fb_lin, hipStream_t st, rtow_stats* stats, float4* accum = nullptr,
+               uint32_t sample_base = 0) {
     auto t0 = std::chrono::steady_clock::now();
     if (!c || !cam) return set_error(RTOW_E_INVALID, "NULL context or camera");
     if (!c->has_scene) return set_error(RTOW_E_INVALID, "no scene uploaded");
     DevParams P;
     int rc = makeParams(c, p, P);
     if (rc) return rc;
+    P.sample_base = sample_base;
     HIP_TRY(hipSetDevice(c->device));
     size_t need = (size_t)P.n_chunks * P.n_local_px * sizeof(float4);
     rc = ensure((void**)&c->d_partial, &c->partial_bytes, std::max<size_t>(need, 16));
@@ -2018,7 +2037,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
     HIP_TRY(hipEventRecord(c->ev[1], st));
     if (P.n_local_px) {
         hipLaunchKernelGGL(resolve_kernel, dim3((P.n_local_px + 255) / 256), dim3(256), 0, st, P, c->d_partial, slab_bgra,
-                           slab_lin, fb_bgra, fb_lin);
+                           slab_lin, fb_bgra, fb_lin, accum);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[2], st));
@@ -2115,6 +2134,7 @@ int rtow_context_destroy(rtow_context* c) {
     if (c->d_work) (void)hipFree(c->d_work);
     if (c->d_partial) (void)hipFree(c->d_partial);
     if (c->d_fb) (void)hipFree(c->d_fb);
+    if (c->d_accum) (void)hipFree(c->d_accum);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2210,6 +2230,50 @@ int rtow_render(rtow_context* c, const rtow_camera* cam, const rtow_params* p, u
     float* d_lin = (float*)(c->d_fb + ((npx * 4 + 255) & ~size_t(255)));
     rc = renderCore(c, cam, &q, nullptr, nullptr, d_bgra, linear_out ? d_lin : nullptr, c->stream, stats);
     if (rc) return rc;
+    if (bgra_out) HIP_TRY(hipMemcpy(bgra_out, d_bgra, npx * 4, hipMemcpyDeviceToHost));
+    if (linear_out) HIP_TRY(hipMemcpy(linear_out, d_lin, npx * 12, hipMemcpyDeviceToHost));
+    return RTOW_OK;
+}
+
+int rtow_render_progressive(rtow_context* c, const rtow_camera* cam, const rtow_params* p, int reset,
+                            uint8_t* bgra_out, float* linear_out, uint32_t* total_spp, rtow_stats* stats) {
+    if (!c || !p || !cam) return set_error(RTOW_E_INVALID, "NULL argument");
+    rtow_params q = *p;
+    q.rank = 0;
+    q.world = 1;
+    // what the accumulated samples were rendered with: camera + every param but spp / chunking
+    rtow_params key = q;
+    key.spp = 0;
+    key.samples_per_chunk = 0;
+    key.blocks_per_cu = 0;
+    key.flags = 0;
+    std::vector<uint8_t> sig(sizeof(rtow_camera) + sizeof(rtow_params));
+    std::memcpy(sig.data(), cam, sizeof(rtow_camera));
+    std::memcpy(sig.data() + sizeof(rtow_camera), &key, sizeof(rtow_params));
+    if (reset || sig != c->accum_sig) {
+        c->accum_spp = 0;
+        c->accum_sig = sig;
+    }
+    if ((uint64_t)c->accum_spp + q.spp > 0xffffffffull) return set_error(RTOW_E_INVALID, "too many accumulated samples");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t npx = (size_t)q.width * q.height;
+    size_t need = npx * 4 + npx * 12 + 256;
+    int rc = ensure((void**)&c->d_fb, &c->fb_bytes, need);
+    if (rc) return rc;
+    const size_t acc_need = (size_t)rtow_rank_tile_count(q.width, q.height, 0, 1) * 64 * sizeof(float4);
+    if (c->accum_bytes < acc_need) c->accum_spp = 0;
+    rc = ensure((void**)&c->d_accum, &c->accum_bytes, acc_need);
+    if (rc) return rc;
+    uint8_t* d_bgra = c->d_fb;
+    float* d_lin = (float*)(c->d_fb + ((npx * 4 + 255) & ~size_t(255)));
+    rc = renderCore(c, cam, &q, nullptr, nullptr, d_bgra, linear_out ? d_lin : nullptr, c->stream, stats, c->d_accum,
+                    c->accum_spp);
+    if (rc) {
+        c->accum_spp = 0;
+        return rc;
+    }
+    c->accum_spp += q.spp;
+    if (total_spp) *total_spp = c->accum_spp;
     if (bgra_out) HIP_TRY(hipMemcpy(bgra_out, d_bgra, npx * 4, hipMemcpyDeviceToHost));
     if (linear_out) HIP_TRY(hipMemcpy(linear_out, d_lin, npx * 12, hipMemcpyDeviceToHost));
     return RTOW_OK;

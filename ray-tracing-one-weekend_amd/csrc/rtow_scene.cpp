@@ -795,6 +795,18 @@ int rtow_camera_main(uint32_t width, uint32_t height, rtow_camera* out) {
     return RTOW_OK;
 }
 
+int rtow_camera_oriented(uint32_t width, uint32_t height, const float look_from[3], const float rows[9],
+                         rtow_camera* out) {
+    if (!out || !look_from || !rows || width == 0 || height == 0)
+        return set_error(RTOW_E_INVALID, "bad camera arguments");
+    Camera c = mainCamera(width, height);
+    c.setOrientationRows(vec3(rows[0], rows[1], rows[2]), vec3(rows[3], rows[4], rows[5]),
+                         vec3(rows[6], rows[7], rows[8]));
+    c.setLookFromPoint(vec3(look_from[0], look_from[1], look_from[2]));
+    *out = c.toDevice();
+    return RTOW_OK;
+}
+
 void rtow_synthetic_image(uint32_t nx, uint32_t ny, uint8_t* rgb) {
     // r = 255*i/(nx-1), g = 255*j/(ny-1), b = 40 + 160*checker32 + (i*j & 31)
     // (tests/scene_io.py:synthetic_image is the same formula)

@@ -98,6 +98,10 @@ def lib():
         "rtow_scene_draws": ([vp], u32),
         "rtow_scene_check": ([vp, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
         "rtow_camera_main": ([u32, u32, ctypes.POINTER(Camera)], i32),
+        "rtow_camera_oriented": ([u32, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                  ctypes.POINTER(Camera)], i32),
+        "rtow_render_progressive": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), i32, vp, vp,
+                                     ctypes.POINTER(u32), ctypes.POINTER(Stats)], i32),
         "rtow_synthetic_image": ([u32, u32, vp], None),
         "rtow_device_count": ([ctypes.POINTER(i32)], i32),
         "rtow_context_create": ([i32, ctypes.POINTER(vp)], i32),
@@ -147,6 +151,15 @@ def camera_main(width, height):
     """The camera main.cpp:111-125 builds for a width x height frame."""
     c = Camera()
     check(lib().rtow_camera_main(width, height, ctypes.byref(c)), "rtow_camera_main")
+    return c
+
+
+def camera_oriented(width, height, look_from, rows):
+    """The main camera after setOrientationMatrix(rows view/east/down) + setLookFromPoint."""
+    lf = (ctypes.c_float * 3)(*look_from)
+    rw = (ctypes.c_float * 9)(*np.asarray(rows, np.float32).reshape(-1))
+    c = Camera()
+    check(lib().rtow_camera_oriented(width, height, lf, rw, ctypes.byref(c)), "rtow_camera_oriented")
     return c
 
 
@@ -266,6 +279,18 @@ class Context:
         check(lib().rtow_render(self._h, ctypes.byref(cam), ctypes.byref(p), bgra.ctypes.data,
                                 lin.ctypes.data if linear else None, ctypes.byref(st)), "rtow_render")
         return bgra, lin, st
+
+    def render_progressive(self, cam, p, reset=False, linear=True):
+        """rtow_render_progressive: p.spp new samples per pixel added to the running
+        sums; returns (bgra, linear or None, total spp, Stats)."""
+        bgra = np.zeros((p.height, p.width, 4), np.uint8)
+        lin = np.zeros((p.height, p.width, 3), np.float32) if linear else None
+        total = ctypes.c_uint32()
+        st = Stats()
+        check(lib().rtow_render_progressive(self._h, ctypes.byref(cam), ctypes.byref(p), 1 if reset else 0,
+                                            bgra.ctypes.data, lin.ctypes.data if linear else None,
+                                            ctypes.byref(total), ctypes.byref(st)), "rtow_render_progressive")
+        return bgra, lin, total.value, st
 
     def trace_sample(self, cam, p, x, y, sample, max_segments=64):
         """rtow_debug_trace_sample: [n, 12] float32 segment records of one sample."""

@@ -1,0 +1,70 @@
+"""Frame-loop pieces: the camera after the GUI loop's updates (pinned against
+the reference's own Camera, tests/golden/make_camera_golden.py) and
+progressive accumulation across frames (rtow_render_progressive)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import rtow
+import scene_io as sio
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CAMS = json.load(open(os.path.join(GOLDEN, "cameras_oriented.json")))
+
+
+@pytest.mark.parametrize("c", CAMS, ids=[c["file"] for c in CAMS])
+def test_oriented_camera_matches_reference(c):
+    cam = rtow.camera_oriented(c["width"], c["height"], c["look_from"], c["rows"])
+    assert bytes(cam) == open(os.path.join(GOLDEN, c["file"]), "rb").read()
+
+
+@pytest.mark.gpu
+def test_progressive_frames_equal_one_render(gpu_ctx):
+    """F frames of S spp == one render of F*S spp with samples_per_chunk S,
+    bit for bit (the random streams continue; the sums add in the same order)."""
+    W, H, S, F = 72, 40, 8, 4
+    scene = rtow.Scene.build("random_ned", n=100, image="synthetic")
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_main(W, H)
+    ref_bgra, ref_lin, _ = gpu_ctx.render(cam, rtow.params(W, H, F * S, seed=3, samples_per_chunk=S))
+    for f in range(F):
+        bgra, lin, total, _ = gpu_ctx.render_progressive(cam, rtow.params(W, H, S, seed=3), reset=(f == 0))
+        assert total == (f + 1) * S
+    assert np.array_equal(lin.view(np.uint32), ref_lin.view(np.uint32))
+    assert np.array_equal(bgra, ref_bgra)
+
+
+@pytest.mark.gpu
+def test_progressive_restarts_on_camera_change(gpu_ctx):
+    W, H = 40, 24
+    scene = rtow.Scene.build("three_sphere")
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, 4, seed=1)
+    gpu_ctx.render_progressive(cam, p, reset=True)
+    _, _, total, _ = gpu_ctx.render_progressive(cam, p)
+    assert total == 8
+    c = CAMS[1]
+    moved = rtow.camera_oriented(W, H, c["look_from"], c["rows"])
+    _, lin, total, _ = gpu_ctx.render_progressive(moved, p)
+    assert total == 4
+    _, one, _ = gpu_ctx.render(moved, p)
+    assert np.array_equal(lin, one)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["random_ned", "cornell"])
+def test_oriented_camera_render_matches_oracle(scene, gpu_ctx):
+    c = CAMS[2]
+    W, H, spp = c["width"], c["height"], 8
+    sc = rtow.Scene.build(scene, n=100, image="synthetic")
+    gpu_ctx.upload(sc)
+    cam = rtow.camera_oriented(W, H, c["look_from"], c["rows"])
+    p = rtow.params(W, H, spp, seed=2)
+    _, lin, _ = gpu_ctx.render(cam, p)
+    olin, _, _ = sio.oracle_render(sc.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                   sio.RtowParams.from_buffer_copy(bytes(p)))
+    rms = np.sqrt(np.mean((lin.reshape(-1, 3).astype(np.float64) - olin) ** 2, axis=0))
+    assert (rms <= 1e-4).all(), rms

@@ -13,7 +13,7 @@ rounds = int(os.environ.get("PROBE_ROUNDS", "2"))
 configs = [("random_ned", 487, 1920, 1080, int(os.environ.get("PROBE_SPP", "32"))), ("cornell_smoke", 100, 800, 800, 32),
            ("cornell", 100, 800, 800, 32), ("final_ned", 100, 1024, 1024, 16)]
 if os.environ.get("PROBE_ONLY"):
-    configs = [c for c in configs if c[0] == os.environ["PROBE_ONLY"]]
+    configs = [c for c in configs if c[0] in os.environ["PROBE_ONLY"].split(",")]
 ctxs = {}
 for w in variants:
     os.environ["RTOW_TRACE_WAVES"] = str(w)
