@@ -244,22 +244,44 @@ __device__ __forceinline__ F3 sph_center(const Sph& s, float time) {
     return add(s.c0, scl(f, s.dc));
 }
 
+// x / a, correctly rounded, from ra = 1/a (itself an IEEE division, hoisted
+// per ray or per sphere): q = x*ra is within 1 ulp of x/a and one FMA
+// residual step rounds it exactly (Markstein's correction; with ra the
+// correctly rounded reciprocal the result equals the IEEE quotient -- checked
+// against every float mantissa at several exponents, 8e9 cases, and 2e8
+// random pairs over the ranges that occur; zero results may differ in sign,
+// which no comparison here sees).  3 VALU instead of the 10 of v_div_scale /
+// v_div_fmas / v_div_fixup.
+__device__ __forceinline__ float div_by(float x, float a, float ra) {
+    const float q0 = x * ra;
+    const float r = fmaf(-q0, a, x);
+    return fmaf(r, ra, q0);
+}
+
+// div_by for a divisor that may be zero (ra = +-inf): x/0 is +-inf and 0/0 NaN,
+// as the IEEE division gives them (the residual is NaN there; q0 is the answer)
+__device__ __forceinline__ float div_by_any(float x, float a, float ra) {
+    const float q0 = x * ra;
+    const float r = fmaf(-q0, a, x);
+    return r == r ? fmaf(r, ra, q0) : q0;
+}
+
 // the root the reference records, strictly inside (tmin, tmax)
 // `a` = dot(d, d) is the same for every sphere a ray meets: hoisted per ray.
-__device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, float a, float tmin, float tmax,
-                                         float& t) {
+__device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, float a, float ra, float tmin,
+                                         float tmax, float& t) {
     const F3 oc = sub(r.o, center);
     const float b = dot(r.d, oc);
     const float c = dot(oc, oc) - radius * radius;
     const float disc = b * b - a * c;
     if (disc > 0) {
         const float sq = sqrtf(disc);
-        const float tn = (-b - sq) / a;
+        const float tn = div_by(-b - sq, a, ra);
         if (tn < tmax && tn > tmin) {
             t = tn;
             return true;
         }
-        const float tf = (-b + sq) / a;
+        const float tf = div_by(-b + sq, a, ra);
         if (tf < tmax && tf > tmin) {
             t = tf;
             return true;
@@ -273,29 +295,30 @@ __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, 
 // the nearer wins and an exact tie goes to the later leaf of the reference
 // tree, i.e. the larger sphere index (see rebuildSah).  `bt`/`best` is the
 // record so far.  The far root is only evaluated when the near one is <= tmin.
-__device__ __forceinline__ bool sph_root(F3 center, float radius, const Ray& r, float a, float tmin, float& t) {
+__device__ __forceinline__ bool sph_root(F3 center, float radius, const Ray& r, float a, float ra, float tmin,
+                                         float& t) {
     const F3 oc = sub(r.o, center);
     const float b = dot(r.d, oc);
     const float c = dot(oc, oc) - radius * radius;
     const float disc = b * b - a * c;
     if (disc > 0) {
         const float sq = sqrtf(disc);
-        float root = (-b - sq) / a;
-        if (!(root < FLT_MAX && root > tmin)) root = (-b + sq) / a;
+        float root = div_by(-b - sq, a, ra);
+        if (!(root < FLT_MAX && root > tmin)) root = div_by(-b + sq, a, ra);
         t = root;
         return root < FLT_MAX && root > tmin;
     }
     return false;
 }
 
-__device__ __forceinline__ bool sph_closer(F3 center, float radius, const Ray& r, float a, float tmin, float bt,
-                                           uint32_t best, uint32_t ref, float& t) {
-    return sph_root(center, radius, r, a, tmin, t) && (t < bt || (t == bt && ref > best));
+__device__ __forceinline__ bool sph_closer(F3 center, float radius, const Ray& r, float a, float ra, float tmin,
+                                           float bt, uint32_t best, uint32_t ref, float& t) {
+    return sph_root(center, radius, r, a, ra, tmin, t) && (t < bt || (t == bt && ref > best));
 }
 
 template <bool UNIT_TIME>
-__device__ __forceinline__ bool sph_t(const Sph& s, const Ray& r, float a, float tmin, float tmax, float& t) {
-    return sph_quad(sph_center<UNIT_TIME>(s, r.time), s.r, r, a, tmin, tmax, t);
+__device__ __forceinline__ bool sph_t(const Sph& s, const Ray& r, float a, float ra, float tmin, float tmax, float& t) {
+    return sph_quad(sph_center<UNIT_TIME>(s, r.time), s.r, r, a, ra, tmin, tmax, t);
 }
 
 // xy_rect.h:22-40, 57-75, 92-110 (closed interval: t == tmax is a hit)
@@ -304,10 +327,11 @@ __device__ __forceinline__ void rect_axes(uint32_t axis, uint32_t& i, uint32_t& 
     j = axis == 0 ? 1u : 2u;
     k = axis == 0 ? 2u : (axis == 1 ? 1u : 0u);
 }
-__device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, float t1, float& t) {
+// inv: the ray's per-axis IEEE reciprocals (SlabRay), so the division is div_by's
+__device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, const F3& inv, float t0, float t1, float& t) {
     uint32_t i, j, k;
     rect_axes(q.axis & 3u, i, j, k);
-    const float tt = (q.k - comp(r.o, k)) / comp(r.d, k);
+    const float tt = div_by_any(q.k - comp(r.o, k), comp(r.d, k), comp(inv, k));
     if (tt < t0 || tt > t1) return false;
     const float x = comp(r.o, i) + tt * comp(r.d, i);
     const float y = comp(r.o, j) + tt * comp(r.d, j);
@@ -319,6 +343,7 @@ __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, float t0, f
 // Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
 struct Prof {
     uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
+    uint32_t disc_pos, accepted, wave_mixed, wave_sph;  // sphere slots with disc > 0 / taken; waves running both slot paths / any sphere path
     unsigned long long cyc_trav, cyc_other;  // wave cycles (s_memtime) in traversal / everything else
 };
 // General scenes: does leaf `cand`, hit at exactly the t of the current best
@@ -344,7 +369,7 @@ __device__ __forceinline__ bool first_active_lane() {
 // Returns the next node to visit, or DK_NONE to pop.
 template <bool UNIT_TIME, int STACK>
 __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
-                                             float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
+                                             float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
                                              uint32_t& overflow) {
     // `best`: in, the current closest leaf; out, the winner of this step's spheres
     const DBvh* n = S.bvh + idx;
@@ -360,7 +385,7 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
     if (hr && rleaf) {
         float t;
         const Sph sp1 = load_sph(S.sph + (lr.y & INDEX_MASK));
-        if (sph_root(sph_center<UNIT_TIME>(sp1, r.time), sp1.r, r, a, tmin, t) &&
+        if (sph_root(sph_center<UNIT_TIME>(sp1, r.time), sp1.r, r, a, ra, tmin, t) &&
             (t < bt || (t == bt && wins_tie(S, lr.y, best)))) {
             bt = t;
             best = lr.y;
@@ -369,7 +394,7 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
     if (hl && lleaf) {
         float t;
         const Sph sp0 = load_sph(S.sph + (lr.x & INDEX_MASK));
-        if (sph_root(sph_center<UNIT_TIME>(sp0, r.time), sp0.r, r, a, tmin, t) &&
+        if (sph_root(sph_center<UNIT_TIME>(sp0, r.time), sp0.r, r, a, ra, tmin, t) &&
             (t < bt || (t == bt && wins_tie(S, lr.x, best)))) {
             bt = t;
             best = lr.x;
@@ -406,11 +431,12 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
                                  float& bt, uint32_t* stk, uint32_t& overflow, Prof& prof) {
     const SlabRay q = slab_ray(r);
     const float a = dot(r.d, r.d);
+    const float ra = 1.0f / a;
     const float time = r.time;
     uint32_t best = mkref(DK_NONE, 0);
     if ((root >> KIND_SHIFT) == DK_SPHERE) {
         float t;
-        if (sph_t<true>(load_sph(S.sph + (root & INDEX_MASK)), r, a, tmin, bt, t)) {
+        if (sph_t<true>(load_sph(S.sph + (root & INDEX_MASK)), r, a, ra, tmin, bt, t)) {
             bt = t;
             best = root;
         }
@@ -427,6 +453,24 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
         const float4* np = reinterpret_cast<const float4*>(nodes + (cur & INDEX_MASK));
         const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
         const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
+        if constexpr (PROF) {
+            const bool sa = (refa >> KIND_SHIFT) == DK_SPHERE, sb = (refb >> KIND_SHIFT) == DK_SPHERE;
+            const unsigned long long act = __ballot(1), ma = __ballot(sa), mb = __ballot(sb);
+            if (first_active_lane()) {
+                prof.wave_mixed += (ma != 0 && ma != act) + (mb != 0 && mb != act);
+                prof.wave_sph += (ma != 0) + (mb != 0);
+            }
+            for (int k = 0; k < 2; k++) {
+                const bool sk = k ? sb : sa;
+                if (!sk) continue;
+                const float4 p0 = k ? b0 : a0, p1 = k ? b1 : a1;
+                const F3 c = add(f3(p0.x, p0.y, p0.z), scl(time, f3(p1.x, p1.y, p1.z)));
+                const F3 oc = sub(r.o, c);
+                const float bq = dot(r.d, oc), cq = dot(oc, oc) - p0.w * p0.w;
+                prof.leaf_tests++;
+                if (bq * bq - a * cq > 0) prof.disc_pos++;
+            }
+        }
         float tb = 0.0f, ta = 0.0f;
         bool hb = false, ha = false;
         // slot b (the right child) first
@@ -434,9 +478,10 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
             // Sphere::hit / MovingSphere::hit with center = c0 + time * (c1 - c0)
             const F3 c = add(f3(b0.x, b0.y, b0.z), scl(time, f3(b1.x, b1.y, b1.z)));
             float t;
-            if (sph_closer(c, b0.w, r, a, tmin, bt, best, refb, t)) {
+            if (sph_closer(c, b0.w, r, a, ra, tmin, bt, best, refb, t)) {
                 bt = t;
                 best = refb;
+                if constexpr (PROF) prof.accepted++;
             }
         } else {
             hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, bt, tb) && (refb >> KIND_SHIFT) == DK_BVH;
@@ -444,9 +489,10 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
             float t;
-            if (sph_closer(c, a0.w, r, a, tmin, bt, best, refa, t)) {
+            if (sph_closer(c, a0.w, r, a, ra, tmin, bt, best, refa, t)) {
                 bt = t;
                 best = refa;
+                if constexpr (PROF) prof.accepted++;
             }
         } else {
             ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, bt, ta) && (refa >> KIND_SHIFT) == DK_BVH;
@@ -523,6 +569,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
     Ray r = chain_ray(S, chain0, wray);
     SlabRay q = slab_ray(r);
     float a = dot(r.d, r.d);
+    float ra = 1.0f / a;
     float bt = tmax;
     bool found = false;
     uint32_t cur = root;
@@ -534,8 +581,8 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             const uint32_t before = found ? best.prim : mkref(DK_NONE, 0);
             uint32_t b = before;
             const uint32_t nxt = S.unit_time
-                                     ? bvh_step<true, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow)
-                                     : bvh_step<false, STACK>(S, idx, r, q, a, tmin, bt, b, stk, sp, overflow);
+                                     ? bvh_step<true, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
+                                     : bvh_step<false, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow);
             if (b != before) {
                 best.prim = b;
                 found = true;
@@ -548,7 +595,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             float t;
             const Sph s = load_sph(S.sph + idx);
             const F3 c = S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time);
-            if (sph_root(c, s.r, r, a, tmin, t) &&
+            if (sph_root(c, s.r, r, a, ra, tmin, t) &&
                 (t < bt || (t == bt && wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0))))) {
                 bt = t;
                 best.prim = cur;
@@ -556,7 +603,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             }
         } else if (kind == DK_RECT) {
             float t;
-            if (rect_t(S.rect[idx], r, tmin, bt, t) &&
+            if (rect_t(S.rect[idx], r, q.inv, tmin, bt, t) &&
                 (t < bt || wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0)))) {
                 bt = t;
                 best.prim = cur;
@@ -588,6 +635,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
                 r = apply_inst(S, cur, r);
                 q = slab_ray(r);
                 a = dot(r.d, r.d);
+                ra = 1.0f / a;
                 cur = I.child;
                 continue;
             }
@@ -596,6 +644,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             r = chain_ray(S, idx, wray);
             q = slab_ray(r);
             a = dot(r.d, r.d);
+            ra = 1.0f / a;
         } else if (kind == DK_MEDIUM) {
             if constexpr (MEDIA) {
                 // constantMedium.h:26-74, called with the list's current closest
@@ -666,7 +715,9 @@ __device__ void finalize(const DevScene& S, uint32_t prim, float t, const Ray& w
     if (kind == DK_SPHERE) {
         const Sph s = load_sph(S.sph + idx);
         rec.p = at(r, t);
-        rec.n = divs(sub(rec.p, S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time)), s.r);
+        const F3 pc = sub(rec.p, S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time));
+        const float rr = 1.0f / s.r;
+        rec.n = f3(div_by(pc.x, s.r, rr), div_by(pc.y, s.r, rr), div_by(pc.z, s.r, rr));
         rec.mat = s.mat;
         if (!s.moving && S.mat[s.mat].needs_uv) sphere_uv(rec.n, rec.u, rec.v);
     } else if (kind == DK_RECT) {
@@ -876,6 +927,58 @@ __device__ __forceinline__ bool decode_pixel(const DevParams& P, uint32_t lp, ui
     return x < P.width && yimg < P.height;
 }
 
+// main.cpp:943-946 + camera.h:123-135 (CAMERA_DOF_EN 0): the sample's jitter,
+// time and primary ray; the counter restarts per sample
+__device__ __forceinline__ void camera_ray(const DevCam& C, const DevParams& P, uint32_t col, uint32_t row,
+                                          uint32_t s, Rng& rng, Ray& ray) {
+    rng.key = rtow_sample_key(P.seed, row * P.width + col, P.sample_base + s);
+    rng.ctr = 0;
+    const float u = (float)((double)col + rng.next()) / (float)P.width;
+    const float v = (float)((double)row + rng.next()) / (float)P.height;
+    const F3 rd = scl(C.lens_radius, f3(1.0f, 1.0f, 1.0f));
+    const F3 offset = add(scl(rd.x, ld3(C.u)), scl(rd.y, ld3(C.v)));
+    const float time = (float)((double)C.t0 + rng.next() * (double)(C.t1 - C.t0));
+    ray.o = add(ld3(C.origin), offset);
+    ray.d = sub(sub(add(add(ld3(C.llc), scl(u, ld3(C.hor))), scl(v, ld3(C.ver))), ld3(C.origin)), offset);
+    ray.time = time;
+}
+
+// The rest of one color() call (color.h:12-59) after the closest hit:
+// scatter into the next segment (done = false) or end the path with its
+// terminal term in `contrib`.
+__device__ __forceinline__ void shade_segment(const DevScene& S, const Tables& T, const DevParams& P, bool hit,
+                                             const Rec& rec, Ray& ray, F3& thr, uint32_t& depth, Rng& rng,
+                                             F3& contrib, bool& done) {
+    done = true;
+    contrib = f3(0, 0, 0);
+    if (hit) {
+        const DMat m = S.mat[rec.mat];
+        Ray sc;
+        F3 att;
+        if (depth < P.max_depth && scatter(S, T, m, ray, rec, rng, att, sc)) {
+            // emitted() is (0,0,0) for every material that scatters
+            // (material.h:38-40; DiffuseLight never scatters), so the
+            // recursion's `emitted + attenuation * color(...)` is a product
+            thr = mulv(thr, att);
+            ray = sc;
+            depth++;
+            done = false;
+        } else if (m.kind == RTOW_MAT_DIFFUSE_LIGHT) {
+            contrib = mulv(thr, tex_value(S, T, m.tex, rec.u, rec.v, rec.p));
+        }
+    } else if (P.gi_enable) {
+        if (depth < 1) {  // color.h:35-50
+            const F3 ud = unit(ray.d);
+            const float t = ud.z;
+            const float rt = (float)(1.0 + t);
+            const F3 sky = f3((float)(rt * 0.1), (float)(rt * 0.3), (float)(rt * 1.0));
+            contrib = mulv(thr, scl(P.sky_gain, sky));
+        } else {
+            contrib = mulv(thr, f3(P.gi_gain, P.gi_gain, P.gi_gain));
+        }
+    }
+}
+
 // MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
 // chain), 2 general scene, 3 general scene with media
 // All LDS is one dynamic region (16-B aligned carve, no static __shared__):
@@ -888,7 +991,7 @@ constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn) {
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
                                                        float4* partial, unsigned long long* counters) {
-    Prof prof{0, 0, 0, 0, 0, 0, 0, 0};
+    Prof prof{};
     unsigned long long t_mark = PROF ? __builtin_amdgcn_s_memtime() : 0;
     constexpr bool SIMPLE = MODE == 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -948,17 +1051,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             }
         }
         if (need_sample) {
-            // main.cpp:943-946 + camera.h:123-135 (CAMERA_DOF_EN 0)
-            rng.key = rtow_sample_key(P.seed, row * P.width + col, P.sample_base + s);
-            rng.ctr = 0;
-            const float u = (float)((double)col + rng.next()) / (float)P.width;
-            const float v = (float)((double)row + rng.next()) / (float)P.height;
-            const F3 rd = scl(C.lens_radius, f3(1.0f, 1.0f, 1.0f));
-            const F3 offset = add(scl(rd.x, ld3(C.u)), scl(rd.y, ld3(C.v)));
-            const float time = (float)((double)C.t0 + rng.next() * (double)(C.t1 - C.t0));
-            ray.o = add(ld3(C.origin), offset);
-            ray.d = sub(sub(add(add(ld3(C.llc), scl(u, ld3(C.hor))), scl(v, ld3(C.ver))), ld3(C.origin)), offset);
-            ray.time = time;
+            camera_ray(C, P, col, row, s, rng, ray);
             thr = f3(1, 1, 1);
             depth = 0;
             need_sample = false;
@@ -1015,34 +1108,9 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 nseg_dbg++;
             }
         }
-        bool done = true;
-        F3 contrib = f3(0, 0, 0);
-        if (hit) {
-            const DMat m = S.mat[rec.mat];
-            Ray sc;
-            F3 att;
-            if (depth < P.max_depth && scatter(S, T, m, ray, rec, rng, att, sc)) {
-                // emitted() is (0,0,0) for every material that scatters
-                // (material.h:38-40; DiffuseLight never scatters), so the
-                // recursion's `emitted + attenuation * color(...)` is a product
-                thr = mulv(thr, att);
-                ray = sc;
-                depth++;
-                done = false;
-            } else if (m.kind == RTOW_MAT_DIFFUSE_LIGHT) {
-                contrib = mulv(thr, tex_value(S, T, m.tex, rec.u, rec.v, rec.p));
-            }
-        } else if (P.gi_enable) {
-            if (depth < 1) {  // color.h:35-50
-                const F3 ud = unit(ray.d);
-                const float t = ud.z;
-                const float rt = (float)(1.0 + t);
-                const F3 sky = f3((float)(rt * 0.1), (float)(rt * 0.3), (float)(rt * 1.0));
-                contrib = mulv(thr, scl(P.sky_gain, sky));
-            } else {
-                contrib = mulv(thr, f3(P.gi_gain, P.gi_gain, P.gi_gain));
-            }
-        }
+        bool done;
+        F3 contrib;
+        shade_segment(S, T, P, hit, rec, ray, thr, depth, rng, contrib, done);
         if (done) {
             acc = add(acc, contrib);
             s++;
@@ -1065,13 +1133,14 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         if (ov) atomicAdd(&counters[1], 1ull);
     }
     if constexpr (PROF) {
-        uint32_t vals[5] = {prof.lane_steps, prof.wave_steps, prof.leaf_tests, prof.lane_iters, prof.wave_iters};
+        uint32_t vals[9] = {prof.lane_steps, prof.wave_steps, prof.leaf_tests, prof.lane_iters, prof.wave_iters,
+                            prof.disc_pos, prof.accepted, prof.wave_mixed, prof.wave_sph};
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < 9; k++) {
             uint32_t x = vals[k];
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-            if (lane == 0) atomicAdd(&counters[2 + k], (unsigned long long)x);
+            if (lane == 0) atomicAdd(&counters[k < 5 ? 2 + k : 4 + k], (unsigned long long)x);
         }
         if (lane == 0) {  // s_memtime is per wave: lane 0's copy is the wave's
             atomicAdd(&counters[7], prof.cyc_trav);
@@ -2041,7 +2110,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[2], st));
-    unsigned long long host_ctr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long host_ctr[13] = {};
     HIP_TRY(hipMemcpyAsync(host_ctr, (uint8_t*)c->d_work + 8, sizeof host_ctr, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (c->profile && host_ctr[3])
@@ -2051,6 +2120,13 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
                      host_ctr[0], host_ctr[2], host_ctr[3], (double)host_ctr[2] / (64.0 * host_ctr[3]),
                      (double)host_ctr[2] / (double)host_ctr[0], host_ctr[5], host_ctr[6],
                      (double)host_ctr[5] / (64.0 * (double)std::max(1ull, host_ctr[6])));
+    if (c->profile && host_ctr[4])
+        std::fprintf(stderr,
+                     "rtow-profile: sphere slots %.2f/ray (disc>0 %.2f, taken %.2f) | per wave step: sphere path %.3f "
+                     "slots, both paths %.3f slots\n",
+                     (double)host_ctr[4] / host_ctr[0], (double)host_ctr[9] / host_ctr[0],
+                     (double)host_ctr[10] / host_ctr[0], (double)host_ctr[12] / host_ctr[3],
+                     (double)host_ctr[11] / host_ctr[3]);
     if (c->profile && host_ctr[7])
         std::fprintf(stderr, "rtow-profile: wave cycles traversal %.3g other %.3g (traversal share %.3f)\n",
                      (double)host_ctr[7], (double)host_ctr[8],

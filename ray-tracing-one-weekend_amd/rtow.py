@@ -118,6 +118,8 @@ def lib():
         "rtow_assemble_device": ([vp, u32, u32, u32, vp, u32, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
+        if not hasattr(L, name) and os.environ.get("RTOW_LIB"):
+            continue  # an older build loaded for A/B comparison (tools/ab.py)
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
