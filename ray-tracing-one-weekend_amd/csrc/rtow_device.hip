@@ -609,6 +609,19 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
                 best.prim = cur;
                 found = true;
             }
+        } else if (kind == DK_RECTS) {
+            // a list of rectangles: scanned in order, closed interval, as hitableList.h
+            const DList R = S.list[idx];
+            for (uint32_t j = 0; j < R.count; j++) {
+                const uint32_t ref = mkref(DK_RECT, R.first + j);
+                float t;
+                if (rect_t(S.rect[R.first + j], r, q.inv, tmin, bt, t) &&
+                    (t < bt || wins_tie(S, ref, found ? best.prim : mkref(DK_NONE, 0)))) {
+                    bt = t;
+                    best.prim = ref;
+                    found = true;
+                }
+            }
         } else if (kind == DK_LIST || kind == DK_LISTNEXT) {
             // items in order; one continuation entry below the item being
             // visited instead of the whole rest of the list
@@ -1339,6 +1352,11 @@ struct ChainAssigner {
             for (uint32_t j = 0; j < l.count; j++) walk(L.refs[l.first + j], depth + 1);
             break;
         }
+        case DK_RECTS: {
+            const DList l = L.list[idx];
+            for (uint32_t j = 0; j < l.count; j++) walk(mkref(DK_RECT, l.first + j), depth + 1);
+            break;
+        }
         case DK_TRANSLATE:
         case DK_ROTY:
         case DK_FLIP:
@@ -1390,13 +1408,14 @@ void assignTieKeys(HostLayout& L, uint32_t ref, std::vector<KeyComp>& path, int 
             path.pop_back();
         }
         break;
-    case DK_LIST: {
+    case DK_LIST:
+    case DK_RECTS: {
         const DList l = L.list[idx];
         uint32_t bits = 1;
         while ((1ull << bits) < 2ull * l.count) bits++;
         for (uint32_t j = 0; j < l.count; j++) {
             path.push_back(KeyComp{bits, (unsigned long long)l.count + j, (unsigned long long)l.count - 1 - j});
-            assignTieKeys(L, L.refs[l.first + j], path, depth + 1);
+            assignTieKeys(L, kind == DK_RECTS ? mkref(DK_RECT, l.first + j) : L.refs[l.first + j], path, depth + 1);
             path.pop_back();
         }
         break;
@@ -1682,11 +1701,19 @@ struct Converter {
             uint32_t first = (uint32_t)L.refs.size();
             L.refs.resize(L.refs.size() + h.b + 1);
             L.refs[first + h.b] = mkref(DK_NONE, 0);  // end of this list's items (DK_LISTNEXT)
+            bool rects = h.b > 0 && h.b <= 16;
             for (uint32_t i = 0; i < h.b; i++) {
                 uint32_t c = conv(s.refs[h.a + i], underBvh);
                 L.refs[first + i] = c;
+                rects = rects && (c >> KIND_SHIFT) == DK_RECT;
             }
             L.list[slot] = DList{first, h.b, 0, 0};
+            if (rects) {  // e.g. a Box's six sides: one fused loop over contiguous leaves
+                const uint32_t r0 = (uint32_t)L.rect.size();
+                for (uint32_t i = 0; i < h.b; i++) L.rect.push_back(L.rect[L.refs[first + i] & INDEX_MASK]);
+                L.list[slot] = DList{r0, h.b, 0, 0};
+                ref = mkref(DK_RECTS, slot);
+            }
             break;
         }
         case RTOW_HIT_BOX:

@@ -32,6 +32,7 @@ enum : uint32_t {
     DK_MEDIUM = 8,
     DK_EXIT = 9,  // traversal-stack marker: leave the innermost instance
     DK_LISTNEXT = 10,  // traversal-stack marker: continue a list at refs[index]
+    DK_RECTS = 11,     // a list of rectangles only (a Box's sides): DList over rect[first, first+count)
     DK_NONE = 15
 };
 
