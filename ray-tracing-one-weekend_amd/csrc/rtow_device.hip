@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -201,17 +202,25 @@ __device__ __forceinline__ SlabRay slab_ray(const Ray& r) {
 
 // Conservative slab test for culling (never the reference's own AABB::hit,
 // whose divisions only decide WHICH subtrees it visits, not the result).
+// The box's exit is widened by |t|*1e-6 (> 2*gamma(3): rounding of the planes);
+// tmax_c is the culling bound, the best hit so far widened by cull_bound().
 __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, float z0, float z1, const SlabRay& q,
-                                     float tmin, float tmax, float& tnear) {
+                                     float tmin, float tmax_c, float& tnear) {
     const float tx0 = (x0 - q.o.x) * q.inv.x, tx1 = (x1 - q.o.x) * q.inv.x;
     const float ty0 = (y0 - q.o.y) * q.inv.y, ty1 = (y1 - q.o.y) * q.inv.y;
     const float tz0 = (z0 - q.o.z) * q.inv.z, tz1 = (z1 - q.o.z) * q.inv.z;
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tf = tf + fabsf(tf) * 1.0e-6f;  // > 2*gamma(3): the reference's exact test can pass where ours rounds out
+    const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    const float tf = fminf(ex + fabsf(ex) * 1.0e-6f, tmax_c);
     tnear = tn;
     return tn <= tf;
 }
+
+// The culling bound for a best hit at t.  A sphere root near tangency carries
+// the cancellation of b*b - a*c: its computed t can sit ~2^-10.5 * t before the
+// ray reaches the sphere's box at all (the reference never culls by the best
+// hit, so it still finds that root).  Boxes are culled only beyond t*(1+2^-9).
+__device__ __forceinline__ float cull_bound(float t) { return t + fabsf(t) * 0.001953125f; }
 
 // ---- spheres: Sphere::hit sphere.h:20-69 and MovingSphere::hit sphere.h:93-118
 struct Sph {
@@ -352,7 +361,7 @@ __device__ __forceinline__ unsigned long long leaf_key(const DevScene& S, uint32
     const uint32_t k = ref >> KIND_SHIFT, i = ref & INDEX_MASK;
     return k == DK_SPHERE ? S.sph_key[i] : (k == DK_RECT ? S.rect_key[i] : (k == DK_MEDIUM ? S.med_key[i] : 0ull));
 }
-__device__ __noinline__ bool wins_tie(const DevScene& S, uint32_t cand, uint32_t best) {
+__device__ __forceinline__ bool wins_tie(const DevScene& S, uint32_t cand, uint32_t best) {
     return (best >> KIND_SHIFT) == DK_NONE || leaf_key(S, cand) > leaf_key(S, best);
 }
 
@@ -378,8 +387,9 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
     const float4 zs = reinterpret_cast<const float4*>(n)[2];
     const uint4 lr = reinterpret_cast<const uint4*>(n)[3];
     float tl, tr;
-    const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, q, tmin, bt, tl);
-    const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, q, tmin, bt, tr);
+    const float btc = cull_bound(bt);
+    const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, q, tmin, btc, tl);
+    const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, q, tmin, btc, tr);
     const bool lleaf = (lr.x >> KIND_SHIFT) == DK_SPHERE;
     const bool rleaf = (lr.y >> KIND_SHIFT) == DK_SPHERE;
     if (hr && rleaf) {
@@ -484,7 +494,7 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, bt, tb) && (refb >> KIND_SHIFT) == DK_BVH;
+            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, cull_bound(bt), tb) && (refb >> KIND_SHIFT) == DK_BVH;
         }
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
@@ -495,7 +505,7 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, bt, ta) && (refa >> KIND_SHIFT) == DK_BVH;
+            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, cull_bound(bt), ta) && (refa >> KIND_SHIFT) == DK_BVH;
         }
         // one back-edge, one exit: push / descend / pop are predicated updates
         const uint32_t NONE = mkref(DK_NONE, 0);
@@ -1527,6 +1537,129 @@ uint32_t sahBuild(const HostLayout& L, std::vector<SahPrim>& P, size_t lo, size_
     return mkref(DK_BVH, idx);
 }
 
+// ---- General scenes: every maximal BvhNode subtree whose leaves all have
+// finite boxes (spheres, Boxes) is rebuilt the same way, over those leaves,
+// as DBvh nodes; exact ties are settled by the tie keys (assigned before, on
+// the reference tree), so the frame does not change.  Leaves keep their
+// instance chains (the rebuild only rearranges the BvhNodes above them).
+struct GenLeaf {
+    float mn[3], mx[3], c[3];
+    uint32_t ref;
+};
+
+void genLeaves(const HostLayout& L, uint32_t ref, std::vector<GenLeaf>& out, bool& bounded, int depth = 0) {
+    const DBvh b = L.bvh[ref & INDEX_MASK];
+    for (int k = 0; k < 2; k++) {
+        const uint32_t child = k ? b.right : b.left;
+        if ((child >> KIND_SHIFT) == DK_BVH && depth < 200) {
+            genLeaves(L, child, out, bounded, depth + 1);
+            continue;
+        }
+        GenLeaf g;
+        const float mn[3] = {b.xs[2 * k], b.ys[2 * k], b.zs[2 * k]};
+        const float mx[3] = {b.xs[2 * k + 1], b.ys[2 * k + 1], b.zs[2 * k + 1]};
+        for (int a = 0; a < 3; a++) {
+            g.mn[a] = mn[a];
+            g.mx[a] = mx[a];
+            if (!(std::fabs(mn[a]) < 1e30f && std::fabs(mx[a]) < 1e30f)) bounded = false;
+            g.c[a] = 0.5f * (mn[a] + mx[a]);
+        }
+        g.ref = child;
+        out.push_back(g);
+    }
+}
+
+uint32_t sahBuildBvh(std::vector<GenLeaf>& P, size_t lo, size_t hi, std::vector<DBvh>& out) {
+    const size_t n = hi - lo;
+    const uint32_t idx = (uint32_t)out.size();
+    out.push_back(DBvh{});
+    int best_axis = 0;
+    size_t best_i = lo + n / 2;
+    double best_cost = DBL_MAX;
+    std::vector<float> right_area(n + 1);
+    auto order = [](int axis) {
+        return [axis](const GenLeaf& x, const GenLeaf& y) {
+            return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.ref < y.ref);
+        };
+    };
+    for (int axis = 0; axis < 3; axis++) {
+        std::sort(P.begin() + lo, P.begin() + hi, order(axis));
+        float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = n; k-- > 1;) {
+            sahUnion(mn, mx, P[lo + k].mn, P[lo + k].mx);
+            right_area[k] = sahArea(mn, mx);
+        }
+        float lmn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lmx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = 1; k < n; k++) {
+            sahUnion(lmn, lmx, P[lo + k - 1].mn, P[lo + k - 1].mx);
+            const double cost = (double)sahArea(lmn, lmx) * (double)k + (double)right_area[k] * (double)(n - k);
+            if (cost < best_cost) {
+                best_cost = cost;
+                best_axis = axis;
+                best_i = lo + k;
+            }
+        }
+    }
+    std::sort(P.begin() + lo, P.begin() + hi, order(best_axis));
+    const size_t range[2][2] = {{lo, best_i}, {best_i, hi}};
+    DBvh d{};
+    uint32_t refs[2];
+    for (int k = 0; k < 2; k++) {
+        const size_t a = range[k][0], b = range[k][1];
+        float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t i = a; i < b; i++) sahUnion(mn, mx, P[i].mn, P[i].mx);
+        d.xs[2 * k] = mn[0];
+        d.xs[2 * k + 1] = mx[0];
+        d.ys[2 * k] = mn[1];
+        d.ys[2 * k + 1] = mx[1];
+        d.zs[2 * k] = mn[2];
+        d.zs[2 * k + 1] = mx[2];
+        refs[k] = b - a == 1 ? P[a].ref : sahBuildBvh(P, a, b, out);
+    }
+    d.left = refs[0];
+    d.right = refs[1];
+    out[idx] = d;
+    return mkref(DK_BVH, idx);
+}
+
+struct GeneralSah {
+    HostLayout& L;
+    uint32_t n_old;  // DBvh nodes of the reference trees (new ones come after)
+    void patch(uint32_t& ref, int depth = 0) {
+        if (depth > 512) return;
+        const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+        switch (kind) {
+        case DK_BVH: {
+            if (idx >= n_old) return;  // already rebuilt (a shared subtree)
+            std::vector<GenLeaf> leaves;
+            bool bounded = true;
+            genLeaves(L, ref, leaves, bounded);
+            for (const GenLeaf& g : leaves) {  // BVHs nested below the leaves
+                uint32_t r = g.ref;
+                patch(r, depth + 1);
+            }
+            if (bounded && leaves.size() >= 2) ref = sahBuildBvh(leaves, 0, leaves.size(), L.bvh);
+            break;
+        }
+        case DK_LIST: {
+            const DList l = L.list[idx];
+            for (uint32_t j = 0; j < l.count; j++) patch(L.refs[l.first + j], depth + 1);
+            break;
+        }
+        case DK_TRANSLATE:
+        case DK_ROTY:
+        case DK_FLIP:
+            patch(L.inst[idx].child, depth + 1);
+            break;
+        case DK_MEDIUM:
+            patch(L.med[idx].boundary, depth + 1);
+            break;
+        default:
+            break;
+        }
+    }
+};
+
 // leaves of the reference tree left to right
 void inorderLeaves(const HostLayout& L, uint32_t ref, std::vector<uint32_t>& out) {
     if ((ref >> KIND_SHIFT) == DK_BVH) {
@@ -1934,6 +2067,12 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     {
         std::vector<KeyComp> path;
         assignTieKeys(L, L.root, path);
+    }
+    if (!L.simple && tree == RTOW_TREE_SAH) {  // after the tie keys: they come from the reference trees
+        GeneralSah g{L, (uint32_t)L.bvh.size()};
+        g.patch(L.root);
+        Bounds bd2{L};
+        L.stack_need = bd2.need(L.root, false).first;
     }
     if (L.sph_key.empty()) L.sph_key.push_back(0);
     if (L.rect_key.empty()) L.rect_key.push_back(0);
