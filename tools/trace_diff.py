@@ -24,7 +24,7 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     scene = args[0] if args else "final_ned"
     W, H, spp = (int(v) for v in args[1:4]) if len(args) >= 4 else (48, 48, 16)
-    d = sio.scene_dict(rtow.Scene.build(scene, image="synthetic"))
+    d = sio.scene_dict(rtow.Scene.build(scene, n=int(os.environ.get("TD_N", "100")), image="synthetic"))
     if "--ground" in sys.argv:  # final_ned's ground item only
         import isolate_ground as ig
         h = d["hitables"]
@@ -34,11 +34,11 @@ def main():
     ctx = rtow.Context(0)
     ctx.upload(sc)
     cam = rtow.camera_main(W, H)
-    p = rtow.params(W, H, spp, seed=5)
+    p = rtow.params(W, H, spp, seed=int(os.environ.get("TD_SEED", "5")))
     ocam = sio.RtowCamera.from_buffer_copy(bytes(cam))
     op = sio.RtowParams.from_buffer_copy(bytes(p))
     _, lin, _ = ctx.render(cam, p)
-    olin, _, _ = sio.oracle_render(sc.view_ptr, ocam, op)
+    olin, _, _ = sio.oracle_render(sc.view_ptr, ocam, op, threads=16)
     diff = np.abs(lin.reshape(-1, 3).astype(np.float64) - olin).max(axis=1)
     bad = np.argsort(-diff)[: int(os.environ.get("TD_PIXELS", "4"))]
     shown = 0
