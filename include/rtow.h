@@ -184,7 +184,7 @@ typedef struct rtow_params {
     uint32_t gi_enable;         /* GLOBAL_ILLUM_EN */
     float sky_gain;             /* SKY_ILLUM_GAIN */
     float gi_gain;              /* GLOBAL_ILLUM_GAIN */
-    uint32_t samples_per_chunk; /* work granularity; 0 = auto (64) */
+    uint32_t samples_per_chunk; /* work granularity; 0 = auto (16, or spp/256 if larger) */
     uint64_t seed;              /* render stream seed (rtow_rng.h) */
     uint32_t rank, world;       /* tile partition; world 0 is treated as 1 */
     uint32_t flags;

@@ -85,6 +85,10 @@ struct Rng {
     __device__ __forceinline__ double next() {
         return (double)rtow_draw24(key, ctr++) * (1.0 / 16777216.0);
     }
+    // the same draw as a float: U = r24 * 2^-24 is exact in float, so
+    // (float)next() == nextf() and a double U compared with, or rounded to,
+    // a float gives what nextf() gives -- without the f64 conversions
+    __device__ __forceinline__ float nextf() { return (float)rtow_draw24(key, ctr++) * (1.0f / 16777216.0f); }
 };
 
 struct DevCam {
@@ -803,45 +807,87 @@ __device__ float perlin_noise(const Tables& T, F3 p) {
     return accum;
 }
 
-__device__ float turbulence(const Tables& T, F3 p) {  // noise.h:38-49
-    float accum = 0;
-    F3 tp = p;
-    float weight = 1.0f;
-    for (int i = 0; i < 7; i++) {
-        accum += weight * perlin_noise(T, tp);
-        weight *= 0.5f;
-        tp = scl(2.0f, tp);
+// Perlin::turbulance (noise.h:38-49), spread over the wave.  Every lane with
+// `want` needs turb(p) = |sum_o 2^-o * noise(2^o p)|, o = 0..6; those 7k
+// octave terms (k lanes) are independent, so the wave's active lanes take
+// them as tasks (task t = 7 * requester + octave) instead of each requester
+// looping over its 7 octaves while the rest of the wave idles.  The terms go
+// through LDS and each requester then sums its own 7 in the reference's order
+// (2^o p is exact, as the reference's repeated tempP *= 2 is, and 2^-o * noise
+// is exactly weight * noise), so the result is bit for bit the loop's.
+// Scratch: this wave's traversal-stack columns, idle between traversals
+// (word q at row q / 64, lane column q % 64; needs STACK * 64 >= 640 words).
+// Must be called by all active lanes of the wave together.
+template <int BS>
+__device__ __forceinline__ float wave_turbulence(const Tables& T, uint32_t* wave_stack, bool want, F3 p) {
+    const unsigned long long wm = __ballot(want);
+    if (wm == 0) return 0.0f;
+    const unsigned long long act = __ballot(1);
+    const uint32_t lane = threadIdx.x & 63u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    auto slot = [&](uint32_t q) -> uint32_t* { return wave_stack + (q >> 6) * BS + (q & 63u); };
+    const uint32_t k = (uint32_t)__popcll(wm);
+    const uint32_t nact = (uint32_t)__popcll(act), ar = (uint32_t)__popcll(act & lt);
+    const uint32_t wr = (uint32_t)__popcll(wm & lt);
+    if (want) {
+        *slot(wr) = __float_as_uint(p.x);
+        *slot(64 + wr) = __float_as_uint(p.y);
+        *slot(128 + wr) = __float_as_uint(p.z);
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t t = ar; t < 7 * k; t += nact) {
+        const uint32_t r = t / 7, o = t - 7 * r;
+        const float sc = (float)(1u << o);
+        const F3 tp = f3(__uint_as_float(*slot(r)) * sc, __uint_as_float(*slot(64 + r)) * sc,
+                         __uint_as_float(*slot(128 + r)) * sc);
+        *slot(192 + t) = __float_as_uint((1.0f / sc) * perlin_noise(T, tp));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    float accum = 0;
+    if (want) {
+#pragma unroll
+        for (uint32_t o = 0; o < 7; o++) accum += __uint_as_float(*slot(192 + 7 * wr + o));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     return fabsf(accum);
 }
 
-__device__ F3 tex_value(const DevScene& S, const Tables& T, uint32_t ti, float u, float v, F3 p) {
+// CheckerTexture (texture.h:23-39) picks one of its textures by position:
+// follow those picks to the texture that gives the value
+__device__ __forceinline__ uint32_t resolve_tex(const DevScene& S, uint32_t ti, F3 p) {
     for (int guard = 0; guard < 32; guard++) {
         const DTex t = S.tex[ti];
-        if (t.kind == RTOW_TEX_CONSTANT) return f3(t.f[0], t.f[1], t.f[2]);
-        if (t.kind == RTOW_TEX_CHECKER) {  // texture.h:27-35
-            const float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
-            ti = sines < 0 ? t.a : t.b;
-            continue;
-        }
-        if (t.kind == RTOW_TEX_NOISE) {  // texture.h:44-48
-            const float s = 1 + sinf(t.f[0] * p.z + 10 * turbulence(T, p));
-            return scl(s, f3(0.5f, 0.5f, 0.5f));
-        }
-        if (t.kind == RTOW_TEX_IMAGE) {  // texture.h:65-79
-            const DImage im = S.img[t.a];
-            const int nx = (int)im.nx, ny = (int)im.ny;
-            const uint8_t* data = S.texels + im.offset;
-            int i = (int)(u * nx);
-            int j = (int)((double)((1 - v) * ny) - 0.001);
-            if (i < 0) i = 0;
-            if (j < 0) j = 0;
-            if (i > nx - 1) i = nx - 1;
-            if (j > ny - 1) j = ny - 1;
-            const size_t o = 3 * (size_t)i + 3 * (size_t)nx * (size_t)j;
-            return f3((float)(data[o] / 255.0), (float)(data[o + 1] / 255.0), (float)(data[o + 2] / 255.0));
-        }
-        break;
+        if (t.kind != RTOW_TEX_CHECKER) break;
+        const float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);  // texture.h:27-35
+        ti = sines < 0 ? t.a : t.b;
+    }
+    return ti;
+}
+
+// Texture::value of a resolved (non-checker) texture; `turb` is
+// Perlin::turbulance(p) when it is a NoiseTexture (wave_turbulence)
+__device__ F3 leaf_tex_value(const DevScene& S, uint32_t ti, float u, float v, F3 p, float turb) {
+    const DTex t = S.tex[ti];
+    if (t.kind == RTOW_TEX_CONSTANT) return f3(t.f[0], t.f[1], t.f[2]);
+    if (t.kind == RTOW_TEX_NOISE) {  // texture.h:44-48
+        const float s = 1 + sinf(t.f[0] * p.z + 10 * turb);
+        return scl(s, f3(0.5f, 0.5f, 0.5f));
+    }
+    if (t.kind == RTOW_TEX_IMAGE) {  // texture.h:65-79
+        const DImage im = S.img[t.a];
+        const int nx = (int)im.nx, ny = (int)im.ny;
+        const uint8_t* data = S.texels + im.offset;
+        int i = (int)(u * nx);
+        int j = (int)((double)((1 - v) * ny) - 0.001);
+        if (i < 0) i = 0;
+        if (j < 0) j = 0;
+        if (i > nx - 1) i = nx - 1;
+        if (j > ny - 1) j = ny - 1;
+        const size_t o = 3 * (size_t)i + 3 * (size_t)nx * (size_t)j;
+        return f3((float)(data[o] / 255.0), (float)(data[o + 1] / 255.0), (float)(data[o + 2] / 255.0));
     }
     return f3(0, 0, 0);
 }
@@ -851,10 +897,10 @@ __device__ F3 tex_value(const DevScene& S, const Tables& T, uint32_t ti, float u
 __device__ __forceinline__ F3 random_in_unit_sphere(Rng& g) {  // mathUtilities.h:19-25
     F3 p;
     do {
-        const double c = g.next();  // g++ evaluates vec3(U, U, U) right to left
-        const double b = g.next();
-        const double a = g.next();
-        p = sub(scl(2.0f, f3((float)a, (float)b, (float)c)), f3(1, 1, 1));
+        const float c = g.nextf();  // g++ evaluates vec3(U, U, U) right to left
+        const float b = g.nextf();
+        const float a = g.nextf();
+        p = sub(scl(2.0f, f3(a, b, c)), f3(1, 1, 1));
     } while (sqlen(p) >= 1.0f);
     return p;
 }
@@ -884,15 +930,15 @@ __device__ __forceinline__ float schlick(float cosine, float ri) {
     return (float)(r0 + (1 - r0) * (x2 * x2 * x));
 }
 
-__device__ bool scatter(const DevScene& S, const Tables& T, const DMat& m, const Ray& in, const Rec& rec, Rng& g,
-                        F3& atten, Ray& out) {
+// tv: the material's texture value at the hit (Lambertian / Isotropic)
+__device__ bool scatter(const DMat& m, const Ray& in, const Rec& rec, F3 tv, Rng& g, F3& atten, Ray& out) {
     switch (m.kind) {
     case RTOW_MAT_LAMBERTIAN: {  // material.h:47-53
         const F3 target = add(add(rec.p, rec.n), random_in_unit_sphere(g));
         out.o = rec.p;
         out.d = sub(target, rec.p);
         out.time = in.time;
-        atten = tex_value(S, T, m.tex, rec.u, rec.v, rec.p);
+        atten = tv;
         return true;
     }
     case RTOW_MAT_METAL: {  // material.h:62-67
@@ -915,7 +961,7 @@ __device__ bool scatter(const DevScene& S, const Tables& T, const DMat& m, const
             cosine = ri * dot(in.d, rec.n) / len(in.d);
         } else {
             outward = rec.n;
-            ni = (float)(1.0 / ri);
+            ni = m.inv_ri;  // (float)(1.0 / ri), computed on the host
             cosine = -dot(in.d, rec.n) / len(in.d);
         }
         if (refract(in.d, outward, ni, refracted))
@@ -924,14 +970,14 @@ __device__ bool scatter(const DevScene& S, const Tables& T, const DMat& m, const
             prob = 1.0f;
         out.o = rec.p;
         out.time = 0.0f;
-        out.d = (g.next() < prob) ? reflected : refracted;
+        out.d = (g.nextf() < prob) ? reflected : refracted;  // double U < (double)prob compares the same reals
         return true;
     }
     case RTOW_MAT_ISOTROPIC: {  // material.h:141-145
         out.o = rec.p;
         out.d = random_in_unit_sphere(g);
         out.time = 0.0f;
-        atten = tex_value(S, T, m.tex, rec.u, rec.v, rec.p);
+        atten = tv;
         return true;
     }
     default:  // DiffuseLight never scatters (material.h:126-128)
@@ -956,29 +1002,58 @@ __device__ __forceinline__ void camera_ray(const DevCam& C, const DevParams& P, 
                                           uint32_t s, Rng& rng, Ray& ray) {
     rng.key = rtow_sample_key(P.seed, row * P.width + col, P.sample_base + s);
     rng.ctr = 0;
-    const float u = (float)((double)col + rng.next()) / (float)P.width;
-    const float v = (float)((double)row + rng.next()) / (float)P.height;
+    // (double)col + U is exact (col < 2^24, U has 24 fraction bits), so its
+    // float rounding is the float sum's (makeParams bounds W and H by 2^24)
+    const float u = ((float)col + rng.nextf()) / (float)P.width;
+    const float v = ((float)row + rng.nextf()) / (float)P.height;
     const F3 rd = scl(C.lens_radius, f3(1.0f, 1.0f, 1.0f));
     const F3 offset = add(scl(rd.x, ld3(C.u)), scl(rd.y, ld3(C.v)));
-    const float time = (float)((double)C.t0 + rng.next() * (double)(C.t1 - C.t0));
+    // with t0 == 0 the double expression is the exact product U*(t1-t0)
+    // rounded once to float, as the float product is (0.0f + keeps -0 -> +0)
+    float time;
+    if (C.t0 == 0.0f)
+        time = 0.0f + rng.nextf() * (C.t1 - C.t0);
+    else
+        time = (float)((double)C.t0 + rng.next() * (double)(C.t1 - C.t0));
     ray.o = add(ld3(C.origin), offset);
     ray.d = sub(sub(add(add(ld3(C.llc), scl(u, ld3(C.hor))), scl(v, ld3(C.ver))), ld3(C.origin)), offset);
     ray.time = time;
 }
 
+// The texture value the hit's material will use: Lambertian / Isotropic
+// albedo when it scatters (material.h:47-53, 141-145), DiffuseLight emission
+// (material.h:130-132); (0,0,0) otherwise.  Texture lookups draw no random
+// numbers, so evaluating them ahead of scatter() changes nothing.  Called by
+// all active lanes together (wave_turbulence).
+template <int BS>
+__device__ __forceinline__ F3 texture_at(const DevScene& S, const Tables& T, const DevParams& P, bool hit,
+                                         const Rec& rec, uint32_t depth, uint32_t* wave_stack) {
+    uint32_t ti = 0;
+    bool need = false;
+    if (hit) {
+        const uint32_t kind = S.mat[rec.mat].kind;
+        need = kind == RTOW_MAT_DIFFUSE_LIGHT ||
+               ((kind == RTOW_MAT_LAMBERTIAN || kind == RTOW_MAT_ISOTROPIC) && depth < P.max_depth);
+        if (need) ti = resolve_tex(S, S.mat[rec.mat].tex, rec.p);
+    }
+    const bool noise = need && S.tex[ti].kind == RTOW_TEX_NOISE;
+    const float turb = wave_turbulence<BS>(T, wave_stack, noise, rec.p);
+    return need ? leaf_tex_value(S, ti, rec.u, rec.v, rec.p, turb) : f3(0, 0, 0);
+}
+
 // The rest of one color() call (color.h:12-59) after the closest hit:
 // scatter into the next segment (done = false) or end the path with its
 // terminal term in `contrib`.
-__device__ __forceinline__ void shade_segment(const DevScene& S, const Tables& T, const DevParams& P, bool hit,
-                                             const Rec& rec, Ray& ray, F3& thr, uint32_t& depth, Rng& rng,
-                                             F3& contrib, bool& done) {
+// tv: the hit material's texture value (texture_at)
+__device__ __forceinline__ void shade_segment(const DevScene& S, const DevParams& P, bool hit, const Rec& rec, F3 tv,
+                                             Ray& ray, F3& thr, uint32_t& depth, Rng& rng, F3& contrib, bool& done) {
     done = true;
     contrib = f3(0, 0, 0);
     if (hit) {
         const DMat m = S.mat[rec.mat];
         Ray sc;
         F3 att;
-        if (depth < P.max_depth && scatter(S, T, m, ray, rec, rng, att, sc)) {
+        if (depth < P.max_depth && scatter(m, ray, rec, tv, rng, att, sc)) {
             // emitted() is (0,0,0) for every material that scatters
             // (material.h:38-40; DiffuseLight never scatters), so the
             // recursion's `emitted + attenuation * color(...)` is a product
@@ -987,7 +1062,7 @@ __device__ __forceinline__ void shade_segment(const DevScene& S, const Tables& T
             depth++;
             done = false;
         } else if (m.kind == RTOW_MAT_DIFFUSE_LIGHT) {
-            contrib = mulv(thr, tex_value(S, T, m.tex, rec.u, rec.v, rec.p));
+            contrib = mulv(thr, tv);
         }
     } else if (P.gi_enable) {
         if (depth < 1) {  // color.h:35-50
@@ -1017,6 +1092,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     Prof prof{};
     unsigned long long t_mark = PROF ? __builtin_amdgcn_s_memtime() : 0;
     constexpr bool SIMPLE = MODE == 0;
+    static_assert(STACK * 64 >= 640, "wave_turbulence scratch lives in the wave's stack columns");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* s_ranvec = reinterpret_cast<float4*>(smem);
     uint32_t* s_perm = reinterpret_cast<uint32_t*>(smem + 4096);
@@ -1133,7 +1209,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         }
         bool done;
         F3 contrib;
-        shade_segment(S, T, P, hit, rec, ray, thr, depth, rng, contrib, done);
+        const F3 tv = texture_at<BS>(S, T, P, hit, rec, depth, stk - lane);
+        shade_segment(S, P, hit, rec, tv, ray, thr, depth, rng, contrib, done);
         if (done) {
             acc = add(acc, contrib);
             s++;
@@ -2023,6 +2100,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         d.kind = m.kind;
         d.tex = m.texture;
         d.param = m.param;
+        d.inv_ri = (float)(1.0 / (double)m.param);
         for (int a = 0; a < 3; a++) d.albedo[a] = m.albedo[a];
         if ((m.kind == RTOW_MAT_LAMBERTIAN || m.kind == RTOW_MAT_DIFFUSE_LIGHT || m.kind == RTOW_MAT_ISOTROPIC) &&
             m.texture >= s.n_textures)
@@ -2196,14 +2274,15 @@ int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32
 
 int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     if (!p || p->width == 0 || p->height == 0 || p->spp == 0) return set_error(RTOW_E_INVALID, "bad params");
-    if ((uint64_t)p->width * p->height > (1ull << 31)) return set_error(RTOW_E_INVALID, "image too large");
+    if ((uint64_t)p->width * p->height > (1ull << 31) || p->width > (1u << 24) || p->height > (1u << 24))
+        return set_error(RTOW_E_INVALID, "image too large");
     uint32_t world = p->world ? p->world : 1;
     if (p->rank >= world) return set_error(RTOW_E_INVALID, "rank >= world");
     std::memset(&P, 0, sizeof P);
     P.width = p->width;
     P.height = p->height;
     P.spp = p->spp;
-    uint32_t spc = p->samples_per_chunk ? p->samples_per_chunk : 64;
+    uint32_t spc = p->samples_per_chunk ? p->samples_per_chunk : 16;  // short items keep the grid's tail short (tools/rank_share.py)
     if (spc > p->spp) spc = p->spp;
     P.n_chunks = (p->spp + spc - 1) / spc;
     if (P.n_chunks > 256 && !p->samples_per_chunk) {

@@ -112,7 +112,8 @@ struct alignas(16) DMedium {  // 16 B, constantMedium.h:21-23
 };
 
 struct alignas(16) DMat {  // 32 B
-    uint32_t kind, tex, needs_uv, pad;
+    uint32_t kind, tex, needs_uv;
+    float inv_ri;  // Dielectric: (float)(1.0 / ref_idx), material.h:97
     float param;
     float albedo[3];
 };

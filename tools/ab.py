@@ -1,6 +1,6 @@
 """A/B two builds of librtow_hip.so in ONE process, interleaved rounds.
 
-  python tools/ab.py A.so B.so [C.so ...]   (AB_SPP, AB_ROUNDS)
+  python tools/ab.py A.so B.so [C.so ...]   (AB_SPP, AB_ROUNDS, AB_SPC, AB_SCENES)
 Each build is loaded through its own copy of rtow.py (RTOW_LIB), renders the
 same frames; images must be identical; the kernel times are compared."""
 import importlib.util
@@ -32,7 +32,11 @@ def main():
     rounds = int(os.environ.get("AB_ROUNDS", "3"))
     mods = [load(f"rtow_{i}", l) for i, l in enumerate(libs)]
     names = [os.path.basename(sp) for sp in specs]
-    configs = [("random_ned", 487, 1920, 1080, spp), ("cornell_smoke", 100, 800, 800, spp)]
+    spc = int(os.environ.get("AB_SPC", "16"))
+    configs = [("random_ned", 487, 1920, 1080, spp), ("cornell_smoke", 100, 800, 800, spp),
+               ("cornell", 100, 800, 800, spp), ("final_ned", 100, 1024, 1024, spp)]
+    only = os.environ.get("AB_SCENES", "random_ned,cornell_smoke").split(",")
+    configs = [c for c in configs if c[0] in only]
     for name, n, W, H, s in configs:
         runs = []
         for m, env in zip(mods, envs):
@@ -46,7 +50,7 @@ def main():
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
-            runs.append((m, sc, ctx, m.camera_main(W, H), m.params(W, H, s, seed=1)))
+            runs.append((m, sc, ctx, m.camera_main(W, H), m.params(W, H, s, seed=1, samples_per_chunk=spc)))
         imgs = [r[2].render(r[3], r[4], linear=True)[1] for r in runs]
         same = all((im == imgs[0]).all() for im in imgs)
         if not same:

@@ -1,5 +1,5 @@
 """One render on cuda:0, timing and segment count, next to the oracle's count
-for small frames.  python tools/one_render.py SCENE W H SPP"""
+for small frames.  python tools/one_render.py SCENE W H SPP  (RTOW_N: random-scene sphere count, default 487)"""
 import os
 import sys
 import time
@@ -9,7 +9,7 @@ sys.path[:0] = [os.path.join(HERE, "..", "tests"), os.path.join(HERE, "..", "ray
 import rtow  # noqa: E402
 import scene_io as sio  # noqa: E402
 
-sc = rtow.Scene.build(sys.argv[1], image="synthetic")
+sc = rtow.Scene.build(sys.argv[1], n=int(os.environ.get("RTOW_N", "487")), image="synthetic")
 ctx = rtow.Context(0)
 ctx.upload(sc)
 W, H, spp = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
