@@ -931,10 +931,16 @@ __device__ __forceinline__ float schlick(float cosine, float ri) {
 }
 
 // tv: the material's texture value at the hit (Lambertian / Isotropic)
+// Lambertian, Metal and Isotropic each start with randomInUnitSphere() and
+// draw nothing else, so one rejection loop serves all three (lanes of a wave
+// with different materials loop together, not one material after another).
 __device__ bool scatter(const DMat& m, const Ray& in, const Rec& rec, F3 tv, Rng& g, F3& atten, Ray& out) {
+    F3 rius = f3(0, 0, 0);
+    if (m.kind == RTOW_MAT_LAMBERTIAN || m.kind == RTOW_MAT_METAL || m.kind == RTOW_MAT_ISOTROPIC)
+        rius = random_in_unit_sphere(g);
     switch (m.kind) {
     case RTOW_MAT_LAMBERTIAN: {  // material.h:47-53
-        const F3 target = add(add(rec.p, rec.n), random_in_unit_sphere(g));
+        const F3 target = add(add(rec.p, rec.n), rius);
         out.o = rec.p;
         out.d = sub(target, rec.p);
         out.time = in.time;
@@ -944,7 +950,7 @@ __device__ bool scatter(const DMat& m, const Ray& in, const Rec& rec, F3 tv, Rng
     case RTOW_MAT_METAL: {  // material.h:62-67
         const F3 reflected = reflect(unit(in.d), rec.n);
         out.o = rec.p;
-        out.d = add(reflected, scl(m.param, random_in_unit_sphere(g)));
+        out.d = add(reflected, scl(m.param, rius));
         out.time = 0.0f;
         atten = ld3(m.albedo);
         return dot(out.d, rec.n) > 0;
@@ -975,7 +981,7 @@ __device__ bool scatter(const DMat& m, const Ray& in, const Rec& rec, F3 tv, Rng
     }
     case RTOW_MAT_ISOTROPIC: {  // material.h:141-145
         out.o = rec.p;
-        out.d = random_in_unit_sphere(g);
+        out.d = rius;
         out.time = 0.0f;
         atten = tv;
         return true;
@@ -2245,6 +2251,8 @@ int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
         if constexpr (MODE == 0 && STACK == 16) {
             if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
             // BVH in LDS: 512-thread blocks, 2 per CU (<= 80 KB LDS each)
+            if (c->lds_nodes == 5 && lds_bytes(STACK, 640, c->scene.n_node, true) <= 80 * 1024)
+                return launchTrace<MODE, STACK, 5, false, 640, true>(c, cam, P, bpc, st);
             if (c->lds_nodes && lds_bytes(STACK, 512, c->scene.n_node, true) <= 80 * 1024)
                 return launchTrace<MODE, STACK, 4, false, 512, true>(c, cam, P, bpc, st);
         }
