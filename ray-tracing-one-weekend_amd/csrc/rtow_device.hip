@@ -2251,8 +2251,6 @@ int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
         if constexpr (MODE == 0 && STACK == 16) {
             if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
             // BVH in LDS: 512-thread blocks, 2 per CU (<= 80 KB LDS each)
-            if (c->lds_nodes == 5 && lds_bytes(STACK, 640, c->scene.n_node, true) <= 80 * 1024)
-                return launchTrace<MODE, STACK, 5, false, 640, true>(c, cam, P, bpc, st);
             if (c->lds_nodes && lds_bytes(STACK, 512, c->scene.n_node, true) <= 80 * 1024)
                 return launchTrace<MODE, STACK, 4, false, 512, true>(c, cam, P, bpc, st);
         }
