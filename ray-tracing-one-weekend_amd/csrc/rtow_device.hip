@@ -572,27 +572,75 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
     return true;
 }
 
+// ConstantMedium::hit (constantMedium.h:26-74) of medium `idx` for the ray
+// `r` in the medium's frame (a = dot(d, d)), called with the list's current
+// closest hit as tmax (hitableList.h:30): true and bt = the scatter distance
+// when the ray scatters inside.  Draws 1 or 2 numbers, as the reference.
+template <bool MEDIA, int STACK>
+__device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
+                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev);
+
+template <int STACK>
+__device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, const Ray& wray,
+                                           float tmin, float& bt, uint32_t* stk, int sp, Rng& rng, uint32_t& overflow) {
+    const DMedium M = S.med[idx];
+    (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
+    float t1 = 0, t2 = 0;
+    bool two;
+    if ((M.boundary >> KIND_SHIFT) == DK_SPHERE) {
+        const Sph s = load_sph(S.sph + (M.boundary & INDEX_MASK));
+        two = S.unit_time ? sphere_boundary<true>(s, r, a, t1, t2) : sphere_boundary<false>(s, r, a, t1, t2);
+    } else {
+        Best b1, b2;
+        two = traverse<false, STACK>(S, M.boundary, wray, M.chain, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow,
+                                     mkref(DK_NONE, 0)) &&
+              traverse<false, STACK>(S, M.boundary, wray, M.chain, (float)((double)b1.t + 0.0001), FLT_MAX, stk, sp,
+                                     rng, b2, overflow, mkref(DK_NONE, 0));
+        t1 = b1.t;
+        t2 = b2.t;
+    }
+    if (two) {
+        float ta = t1, tb = t2;
+        if (ta < tmin) ta = tmin;
+        if (tb > bt) tb = bt;
+        if (!(ta >= tb)) {
+            if (ta < 0) ta = 0;
+            const float dl = len(r.d);
+            const float inside = (tb - ta) * dl;
+            const float dist = (float)(-(1 / M.density) * log(rng.next()));
+            if (dist < inside) {
+                bt = ta + dist / dl;
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
 // Closest hit of `root` for a world-space ray, reference semantics, any scene
 // graph: lists in order with a shrinking tmax (hitableList.h:20-38),
 // instances, rectangles, media; exact ties settled by the tie keys.
 // `r` is the ray in the frame of chain `chain0` (the frame `root` sits in).
 // stk: this lane's LDS stack column.
+// `prev`: the leaf that holds tmax from before the call (DK_NONE: none), for
+// exact ties at tmax.
 template <bool MEDIA, int STACK>
 __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
-                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow) {
+                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev) {
     Ray r = chain_ray(S, chain0, wray);
     SlabRay q = slab_ray(r);
     float a = dot(r.d, r.d);
     float ra = 1.0f / a;
     float bt = tmax;
     bool found = false;
+    best.prim = prev;
     uint32_t cur = root;
     int sp = sp0;
     while (true) {
         uint32_t kind = cur >> KIND_SHIFT;
         const uint32_t idx = cur & INDEX_MASK;
         if (kind == DK_BVH) {
-            const uint32_t before = found ? best.prim : mkref(DK_NONE, 0);
+            const uint32_t before = best.prim;
             uint32_t b = before;
             const uint32_t nxt = S.unit_time
                                      ? bvh_step<true, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
@@ -610,7 +658,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             const Sph s = load_sph(S.sph + idx);
             const F3 c = S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time);
             if (sph_root(c, s.r, r, a, ra, tmin, t) &&
-                (t < bt || (t == bt && wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0))))) {
+                (t < bt || (t == bt && wins_tie(S, cur, best.prim)))) {
                 bt = t;
                 best.prim = cur;
                 found = true;
@@ -618,7 +666,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
         } else if (kind == DK_RECT) {
             float t;
             if (rect_t(S.rect[idx], r, q.inv, tmin, bt, t) &&
-                (t < bt || wins_tie(S, cur, found ? best.prim : mkref(DK_NONE, 0)))) {
+                (t < bt || wins_tie(S, cur, best.prim))) {
                 bt = t;
                 best.prim = cur;
                 found = true;
@@ -630,7 +678,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
                 const uint32_t ref = mkref(DK_RECT, R.first + j);
                 float t;
                 if (rect_t(S.rect[R.first + j], r, q.inv, tmin, bt, t) &&
-                    (t < bt || wins_tie(S, ref, found ? best.prim : mkref(DK_NONE, 0)))) {
+                    (t < bt || wins_tie(S, ref, best.prim))) {
                     bt = t;
                     best.prim = ref;
                     found = true;
@@ -674,39 +722,9 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             ra = 1.0f / a;
         } else if (kind == DK_MEDIUM) {
             if constexpr (MEDIA) {
-                // constantMedium.h:26-74, called with the list's current closest
-                // hit as tmax (hitableList.h:30)
-                const DMedium M = S.med[idx];
-                (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
-                float t1 = 0, t2 = 0;
-                bool two;
-                if ((M.boundary >> KIND_SHIFT) == DK_SPHERE) {
-                    const Sph s = load_sph(S.sph + (M.boundary & INDEX_MASK));
-                    two = S.unit_time ? sphere_boundary<true>(s, r, a, t1, t2) : sphere_boundary<false>(s, r, a, t1, t2);
-                } else {
-                    Best b1, b2;
-                    two = traverse<false, STACK>(S, M.boundary, wray, M.chain, -FLT_MAX, FLT_MAX, stk, sp, rng, b1,
-                                                 overflow) &&
-                          traverse<false, STACK>(S, M.boundary, wray, M.chain, (float)((double)b1.t + 0.0001), FLT_MAX,
-                                                 stk, sp, rng, b2, overflow);
-                    t1 = b1.t;
-                    t2 = b2.t;
-                }
-                if (two) {
-                    float ta = t1, tb = t2;
-                    if (ta < tmin) ta = tmin;
-                    if (tb > bt) tb = bt;
-                    if (!(ta >= tb)) {
-                        if (ta < 0) ta = 0;
-                        const float dl = len(r.d);
-                        const float inside = (tb - ta) * dl;
-                        const float dist = (float)(-(1 / M.density) * log(rng.next()));
-                        if (dist < inside) {
-                            bt = ta + dist / dl;
-                            best.prim = cur;
-                            found = true;
-                        }
-                    }
+                if (medium_hit<STACK>(S, idx, r, a, wray, tmin, bt, stk, sp, rng, overflow)) {
+                    best.prim = cur;
+                    found = true;
                 }
             }
         }
@@ -715,6 +733,69 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
         cur = stk[sp * BLOCK];
     }
     best.t = bt;
+    return found;
+}
+
+// The closest hit of a general scene whose root (below its instances) is a
+// list, scanned as hitableList.h:20-38 does: items in order, tmax the closest
+// hit so far.  The loop is uniform across the wave (see DTop).
+template <bool MEDIA, int STACK>
+__device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
+                             uint32_t& overflow) {
+    float bt = FLT_MAX;
+    uint32_t bp = mkref(DK_NONE, 0);
+    bool found = false;
+    // per-direction constants, recomputed only when a chain turns the ray
+    bool have = false;
+    uint32_t dx = 0, dy = 0, dz = 0;
+    F3 inv = f3(0, 0, 0);
+    float a = 0, ra = 0;
+    const uint32_t n = S.n_top ? S.n_top : 1u;  // no top-level list: the whole graph is one item
+    for (uint32_t j = 0; j < n; j++) {
+        const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
+        if (T.kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
+            Best b;
+            if (traverse<MEDIA, STACK>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp)) {
+                bt = b.t;
+                bp = b.prim;
+                found = true;
+            }
+            continue;
+        }
+        const Ray r = chain_ray(S, T.chain, wray);
+        if (!have || __float_as_uint(r.d.x) != dx || __float_as_uint(r.d.y) != dy || __float_as_uint(r.d.z) != dz) {
+            have = true;
+            dx = __float_as_uint(r.d.x);
+            dy = __float_as_uint(r.d.y);
+            dz = __float_as_uint(r.d.z);
+            inv = inv_dir(r.d);
+            a = dot(r.d, r.d);
+            ra = 1.0f / a;
+        }
+        if (T.kind == TOP_RECTS) {
+            for (uint32_t k = 0; k < T.b; k++) {
+                const uint32_t ref = mkref(DK_RECT, T.a + k);
+                float t;
+                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, bp))) {
+                    bt = t;
+                    bp = ref;
+                    found = true;
+                }
+            }
+        } else if (T.kind == TOP_SPHERE) {
+            const uint32_t ref = mkref(DK_SPHERE, T.a);
+            const Sph sp = load_sph(S.sph + T.a);
+            const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
+            float t;
+            if (sph_root(c, sp.r, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, ref, bp)))) {
+                bt = t;
+                bp = ref;
+                found = true;
+            }
+        }
+    }
+    best.t = bt;
+    best.prim = bp;
     return found;
 }
 
@@ -1189,7 +1270,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         } else {
             Best best;
             best.prim = 0;
-            hit = traverse<MODE == 3, STACK>(S, S.root, ray, 0u, 0.001f, FLT_MAX, stk, 0, rng, best, overflow);
+            hit = traverse_top<MODE == 3, STACK>(S, ray, 0.001f, stk, rng, best, overflow);
             if (hit) finalize<false>(S, best.prim, best.t, ray, rec);
         }
         if constexpr (DBG) {
@@ -1363,6 +1444,7 @@ struct HostLayout {
     uint32_t bvh_root = 0;
     std::vector<unsigned long long> sph_key, rect_key, med_key;
     std::vector<DChain> chains;
+    std::vector<DTop> top;
 };
 
 // ---------------------------------------------------------------------------
@@ -2214,6 +2296,56 @@ struct Bounds {
     }
 };
 
+// DTop descriptors of a general scene whose root, below its instances, is a
+// list (empty otherwise)
+void buildTop(HostLayout& L) {
+    L.top.clear();
+    std::vector<uint32_t> path;
+    uint32_t ref = L.root;
+    for (int guard = 0; guard < 64; guard++) {
+        const uint32_t k = ref >> KIND_SHIFT;
+        if (k != DK_TRANSLATE && k != DK_ROTY && k != DK_FLIP) break;
+        path.push_back(ref);
+        ref = L.inst[ref & INDEX_MASK].child;
+    }
+    if ((ref >> KIND_SHIFT) != DK_LIST) return;
+    uint32_t list_chain = ~0u;
+    for (uint32_t c = 0; c < L.chains.size(); c++) {
+        const DChain& C = L.chains[c];
+        if (C.n != path.size()) continue;
+        bool same = true;
+        for (uint32_t k = 0; k < C.n; k++) same = same && C.ref[k] == path[k];
+        if (same) {
+            list_chain = c;
+            break;
+        }
+    }
+    if (list_chain == ~0u) return;
+    const DList l = L.list[ref & INDEX_MASK];
+    for (uint32_t j = 0; j < l.count; j++) {
+        const uint32_t item = L.refs[l.first + j];
+        uint32_t leaf = item;
+        for (int guard = 0; guard < 64; guard++) {
+            const uint32_t k = leaf >> KIND_SHIFT;
+            if (k != DK_TRANSLATE && k != DK_ROTY && k != DK_FLIP) break;
+            leaf = L.inst[leaf & INDEX_MASK].child;
+        }
+        const uint32_t k = leaf >> KIND_SHIFT, i = leaf & INDEX_MASK;
+        DTop t{TOP_GENERIC, item, 0, list_chain};
+        if (k == DK_RECT) {
+            t = DTop{TOP_RECTS, i, 1, L.rect[i].chain};
+        } else if (k == DK_RECTS) {
+            const DList& r = L.list[i];
+            bool one = r.count > 0;
+            for (uint32_t q = 1; q < r.count; q++) one = one && L.rect[r.first + q].chain == L.rect[r.first].chain;
+            if (one) t = DTop{TOP_RECTS, r.first, r.count, L.rect[r.first].chain};
+        } else if (k == DK_SPHERE) {
+            t = DTop{TOP_SPHERE, i, 0, L.sph[i].chain};
+        }
+        L.top.push_back(t);
+    }
+}
+
 bool textureNeedsUv(const rtow_scene& s, uint32_t ti, int guard = 0) {
     if (ti >= s.n_textures || guard > 32) return false;
     const rtow_texture& t = s.textures[ti];
@@ -2343,6 +2475,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         Bounds bd2{L};
         L.stack_need = bd2.need(L.root, false).first;
     }
+    if (!L.simple) buildTop(L);
     if (L.sph_key.empty()) L.sph_key.push_back(0);
     if (L.rect_key.empty()) L.rect_key.push_back(0);
     if (L.med_key.empty()) L.med_key.push_back(0);
@@ -2685,6 +2818,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_img = pushBlob(blob, L.img), o_texels = pushBlob(blob, L.texels);
     size_t o_ch = pushBlob(blob, L.chains);
     size_t o_ks = pushBlob(blob, L.sph_key), o_kr = pushBlob(blob, L.rect_key), o_km = pushBlob(blob, L.med_key);
+    std::vector<DTop> top = L.top;
+    if (top.empty()) top.push_back(DTop{});
+    size_t o_top = pushBlob(blob, top);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2714,6 +2850,8 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.sph_key = (const unsigned long long*)(b + o_ks);
     d.rect_key = (const unsigned long long*)(b + o_kr);
     d.med_key = (const unsigned long long*)(b + o_km);
+    d.top = (const DTop*)(b + o_top);
+    d.n_top = (uint32_t)L.top.size();
     d.root = L.root;
     d.stack_need = L.stack_need;
     d.has_media = L.has_media ? 1u : 0u;

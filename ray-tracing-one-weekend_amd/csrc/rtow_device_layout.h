@@ -111,6 +111,21 @@ struct alignas(16) DMedium {  // 16 B, constantMedium.h:21-23
     uint32_t chain;
 };
 
+// The top-level list of a general scene (below the root's instances), as the
+// kernel scans it: item by item with the whole wave on the same item, so the
+// descriptors are read with uniform (scalar) loads and the wave stays
+// together.  An item that is a chain of instances over one sphere, one
+// rectangle or a Box's rectangles is tested in place (the leaf's chain gives
+// the ray in the leaf's frame); anything else (media too) goes to the
+// general traversal.
+enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2 };
+struct alignas(16) DTop {  // 16 B
+    uint32_t kind;
+    uint32_t a;      // GENERIC: item ref; RECTS: first rectangle; SPHERE: sphere
+    uint32_t b;      // RECTS: count
+    uint32_t chain;  // the chain of the leaf's frame (GENERIC: of the list's frame)
+};
+
 struct alignas(16) DMat {  // 32 B
     uint32_t kind, tex, needs_uv;
     float inv_ri;  // Dielectric: (float)(1.0 / ref_idx), material.h:97
@@ -139,6 +154,8 @@ struct DevScene {
     const uint32_t* refs;
     const DMedium* med;
     const DChain* chains;
+    const DTop* top;         // general scenes: the top-level list, n_top items (0: none)
+    uint32_t n_top;
     // Tie keys (general scenes): per sphere / rectangle / medium leaf, the
     // order in which the reference settles an exact tie in t (see
     // assignTieKeys in rtow_device.hip): the larger key wins.
