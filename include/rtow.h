@@ -184,7 +184,8 @@ typedef struct rtow_params {
     uint32_t gi_enable;         /* GLOBAL_ILLUM_EN */
     float sky_gain;             /* SKY_ILLUM_GAIN */
     float gi_gain;              /* GLOBAL_ILLUM_GAIN */
-    uint32_t samples_per_chunk; /* work granularity; 0 = auto (16, or spp/256 if larger) */
+    uint32_t samples_per_chunk; /* work granularity; 0 = auto (16, or spp/200 if larger, with the last
+                                    spc..2spc samples cut into halving chunks) */
     uint64_t seed;              /* render stream seed (rtow_rng.h) */
     uint32_t rank, world;       /* tile partition; world 0 is treated as 1 */
     uint32_t flags;
@@ -283,14 +284,16 @@ int rtow_scene_check(const rtow_scene* scene, uint32_t* stack_need, uint32_t* ch
 /* Convert the scene graph to the device layout and copy it to HBM. */
 int rtow_scene_upload(rtow_context* ctx, const rtow_scene* scene);
 
-/* Acceleration tree the device traverses for a scene made of BvhNodes and
- * spheres only (taking effect at the next rtow_scene_upload).  The closest
- * hit does not depend on it: exact ties are settled by the reference tree's
- * leaf order (BvhNode::hit, bvhNode.h:74-77) either way, so both give the
- * same frame.  SAH (default): a surface-area-heuristic tree rebuilt over the
- * same spheres.  REFERENCE: the reference's own random-axis median-split tree
- * (bvhNode.h:25-59).  Other scenes always use the reference tree.  The
- * environment variable RTOW_BVH=ref|sah overrides the default at context
+/* How the device organises the world (taking effect at the next
+ * rtow_scene_upload).  The closest hit does not depend on it: exact ties are
+ * settled by the reference's own evaluation order (BvhNode::hit,
+ * bvhNode.h:74-77; HitableList::hit, hitableList.h:20-38) either way, so both
+ * give the same frame.  SAH (default): surface-area-heuristic trees rebuilt
+ * over the leaves of every BvhNode subtree and over runs of list items that
+ * hold a large aggregate, and the top-level list scanned item by item.
+ * REFERENCE: the reference's own random-axis median-split trees
+ * (bvhNode.h:25-59) and lists, traversed as the object graph nests them.
+ * The environment variable RTOW_BVH=ref|sah overrides the default at context
  * creation. */
 enum {
     RTOW_TREE_SAH = 0,
@@ -314,8 +317,9 @@ int rtow_render(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
  * The sums restart when `reset` is set or the camera or any parameter other
  * than spp / samples_per_chunk / blocks_per_cu / flags changed.  total_spp
  * (may be NULL) receives the samples per pixel accumulated.  F frames of S
- * spp give the frame of one rtow_render of F*S spp with samples_per_chunk = S,
- * bit for bit. */
+ * spp, each one chunk (samples_per_chunk = S, or automatic chunking with
+ * S <= 16), give the frame of one rtow_render of F*S spp with
+ * samples_per_chunk = S, bit for bit. */
 int rtow_render_progressive(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p, int reset,
                             uint8_t* bgra_out, float* linear_out, uint32_t* total_spp, rtow_stats* stats);
 

@@ -96,9 +96,17 @@ struct DevCam {
     float lens_radius, t0, t1;
 };
 
+// Chunks of a pixel's samples (one work item = one chunk of one pixel): n_big
+// chunks of spc samples (the last one shorter when there is no tail), then,
+// for auto chunking, a tail of R = spp - n_big*spc samples (spc <= R < 2 spc)
+// cut into halving chunks: tail chunk k holds samples
+// [base + R - L(k), base + R - L(k+1)), L(k) = ceil(R / 2^k), L(n_tail) = 0 --
+// R = 16 gives 8, 4, 2, 1, 1.  Items run chunk-major, so the grid ends on
+// one-sample items instead of spc-sample ones: a short tail at every rank count.
 struct DevParams {
     uint32_t width, height, spp, spc;  // spc: samples per chunk
     uint32_t n_chunks, n_local_px, tiles_x, rank, world;
+    uint32_t n_big, tail_r, n_tail;
     uint32_t max_depth, gi_enable;
     float sky_gain, gi_gain;
     uint64_t seed;
@@ -1229,8 +1237,16 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 if (!decode_pixel(P, lp, x, yimg)) continue;  // padding pixel of a partial tile
                 col = x;
                 row = P.height - 1u - yimg;  // reference row numbering (main.cpp:932)
-                s = chunk * P.spc;
-                s_end = min(s + P.spc, P.spp);
+                if (chunk < P.n_big) {
+                    s = chunk * P.spc;
+                    s_end = min(s + P.spc, P.spp);
+                } else {
+                    const uint32_t k = chunk - P.n_big, base = P.n_big * P.spc, R = P.tail_r;
+                    const uint32_t lk = (R + (1u << k) - 1u) >> k;
+                    const uint32_t lk1 = k + 1 == P.n_tail ? 0u : (R + (2u << k) - 1u) >> (k + 1);
+                    s = base + R - lk;
+                    s_end = base + R - lk1;
+                }
                 acc = f3(0, 0, 0);
                 need_item = false;
                 need_sample = true;
@@ -2475,7 +2491,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         Bounds bd2{L};
         L.stack_need = bd2.need(L.root, false).first;
     }
-    if (!L.simple) buildTop(L);
+    if (!L.simple && tree == RTOW_TREE_SAH) buildTop(L);
     if (L.sph_key.empty()) L.sph_key.push_back(0);
     if (L.rect_key.empty()) L.rect_key.push_back(0);
     if (L.med_key.empty()) L.med_key.push_back(0);
@@ -2609,11 +2625,20 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     uint32_t spc = p->samples_per_chunk ? p->samples_per_chunk : 16;  // short items keep the grid's tail short (tools/rank_share.py)
     if (spc > p->spp) spc = p->spp;
     P.n_chunks = (p->spp + spc - 1) / spc;
-    if (P.n_chunks > 256 && !p->samples_per_chunk) {
-        spc = (p->spp + 255) / 256;
+    if (P.n_chunks > 200 && !p->samples_per_chunk) {
+        spc = (p->spp + 199) / 200;
         P.n_chunks = (p->spp + spc - 1) / spc;
     }
     P.spc = spc;
+    P.n_big = P.n_chunks;
+    if (!p->samples_per_chunk && p->spp >= 2 * spc) {  // auto: halving tail (DevParams)
+        P.n_big = (p->spp - spc) / spc;
+        P.tail_r = p->spp - P.n_big * spc;
+        uint32_t k = 0;
+        while (((P.tail_r + (1u << k) - 1u) >> k) > 1u) k++;
+        P.n_tail = k + 1;
+        P.n_chunks = P.n_big + P.n_tail;
+    }
     P.tiles_x = (p->width + 7) / 8;
     P.rank = p->rank;
     P.world = world;

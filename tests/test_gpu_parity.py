@@ -85,7 +85,7 @@ def test_tile_partition_is_bitwise_invariant(world, gpu_ctx):
     assert np.array_equal(frame.cpu().numpy(), full)
 
 
-@pytest.mark.parametrize("W,H,spp,chunk", [(1, 1, 3, 0), (13, 7, 100, 0), (9, 9, 5, 2), (8, 8, 64, 64)])
+@pytest.mark.parametrize("W,H,spp,chunk", [(1, 1, 3, 0), (13, 7, 100, 0), (9, 9, 5, 2), (8, 8, 64, 64), (5, 3, 1000, 0)])
 def test_ragged_sizes_and_chunking(W, H, spp, chunk, gpu_ctx):
     scene = rtow.Scene.build("random_ned", n=100, image="none")
     gpu_ctx.upload(scene)
@@ -170,13 +170,14 @@ def test_full_frame_every_pixel_against_oracle(gpu_ctx):
 
 
 @pytest.mark.parametrize("scene,n", [("random_ned", 487), ("random_ned", 100), ("three_sphere", 0),
-                                     ("final_ned", 0), ("cornell_smoke", 0)])
+                                     ("final_ned", 0), ("cornell_smoke", 0), ("cornell", 0)])
 def test_tree_does_not_change_the_frame(scene, n):
-    """The SAH trees (default; simple scenes: DNodes, general scenes: every
-    BvhNode subtree over bounded leaves) and the reference's own BvhNode trees
-    give the same frame bit for bit: the closest hit is a property of the
-    leaves, and exact ties follow the reference's order in both (final_ned's
-    coplanar box sides tie thousands of times)."""
+    """The SAH organisation (default; simple scenes: DNodes; general scenes:
+    every BvhNode subtree over bounded leaves, trees over runs of list items
+    around media, the top-level list scanned item by item) and the reference's
+    own BvhNode trees and lists give the same frame bit for bit: the closest
+    hit is a property of the leaves, and exact ties follow the reference's
+    order in both (final_ned's coplanar box sides tie thousands of times)."""
     W, H, spp = 96, 54, 16
     sc = rtow.Scene.build(scene, n=max(n, 1), image="synthetic")
     cam = rtow.camera_main(W, H)
