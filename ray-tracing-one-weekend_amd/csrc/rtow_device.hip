@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -2561,9 +2562,22 @@ int ensure(void** p, size_t* have, size_t need) {
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const size_t lds = lds_bytes(STACK, BS, c->scene.n_node, LDSN);
+    // the occupancy query is host work between the launch events: once per
+    // (kernel, LDS size) per process
+    static std::mutex mu;
+    static std::map<std::pair<int, size_t>, int> occ_cache;
     int occ = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>,
-                                                         BS, lds));
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = occ_cache.find({c->device, lds});
+        if (it != occ_cache.end()) {
+            occ = it->second;
+        } else {
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &occ, trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>, BS, lds));
+            occ_cache[{c->device, lds}] = occ;
+        }
+    }
     if (occ < 1) occ = 1;
     uint32_t per = bpc ? bpc : (uint32_t)occ;
     uint32_t grid = (uint32_t)c->cus * per;
