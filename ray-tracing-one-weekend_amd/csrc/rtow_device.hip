@@ -1701,6 +1701,16 @@ uint32_t sahBuild(const HostLayout& L, std::vector<SahPrim>& P, size_t lo, size_
         }
         refs[k] = b - a == 1 ? P[a].ref : sahBuild(L, P, a, b, out, needs[k], depth + 1);
     }
+    // A node with one sphere child keeps it in slot b: the kernel runs a
+    // slot's sphere path (or box path) once for every lane of the wave that
+    // needs it, so slot b's box path is left to inner-inner nodes and slot
+    // a's sphere path to sphere-sphere nodes.  (Slots carry no order: ties go
+    // by sphere index and the nearer inner child is visited first.)  +2 %.
+    if ((refs[0] >> KIND_SHIFT) == DK_SPHERE && (refs[1] >> KIND_SHIFT) != DK_SPHERE) {
+        std::swap(refs[0], refs[1]);
+        std::swap(needs[0], needs[1]);
+        for (int q = 0; q < 6; q++) std::swap(box[0][q], box[1][q]);
+    }
     DNode& d = out[idx];
     for (int k = 0; k < 2; k++) {
         float* f = k == 0 ? d.a : d.b;
