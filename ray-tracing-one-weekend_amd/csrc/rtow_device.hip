@@ -46,7 +46,10 @@
 
 using namespace rtow_dev;
 
-namespace {
+// Device code lives in a named namespace so that one kernel instantiation can
+// come from a second compilation of this file with its own code-generation
+// flags (RTOW_TU_SIMPLE, see the Makefile and the end of this section).
+namespace rtow_k {
 
 constexpr int BLOCK = 256;
 constexpr int ROOTCHAIN = 4;  // DevScene::root_chain (simple scenes)
@@ -1356,6 +1359,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
 // accum (progressive frames, single rank): running per-pixel sums of all
 // frames; this frame's chunk sums are added to it in order, and the average
 // is over P.sample_base + P.spp samples.
+#ifndef RTOW_TU_SIMPLE
 __global__ void resolve_kernel(DevParams P, const float4* partial, uint8_t* slab_bgra, float* slab_lin,
                                uint8_t* fb_bgra, float* fb_lin, float4* accum) {
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1420,7 +1424,22 @@ __global__ void assemble_kernel(uint32_t W, uint32_t H, uint32_t world, uint32_t
     fb[i] = slabs[(size_t)rank * stride_px + slot * 64u + (y & 7u) * 8u + (x & 7u)];
 }
 
-}  // namespace
+#endif  // RTOW_TU_SIMPLE
+
+// The simple-scene kernel the bench runs (random scene, BVH in LDS) is
+// compiled in its own translation unit with -amdgpu-sched-strategy=
+// iterative-ilp (+2.8 % there, but -3..-6 % on the general kernels).
+#define RTOW_SIMPLE_HOT_ARGS DevScene, DevCam, DevParams, uint32_t*, float4*, unsigned long long*
+#ifdef RTOW_TU_SIMPLE
+template __global__ void trace_kernel<0, 16, 4, false, 512, true, false>(RTOW_SIMPLE_HOT_ARGS);
+#else
+extern template __global__ void trace_kernel<0, 16, 4, false, 512, true, false>(RTOW_SIMPLE_HOT_ARGS);
+#endif
+
+}  // namespace rtow_k
+using namespace rtow_k;
+
+#ifndef RTOW_TU_SIMPLE
 
 // ===========================================================================
 // host side: scene conversion, context, C-ABI
@@ -3031,3 +3050,4 @@ int rtow_assemble_device(rtow_context* c, uint32_t width, uint32_t height, uint3
 }
 
 }  // extern "C"
+#endif  // RTOW_TU_SIMPLE
