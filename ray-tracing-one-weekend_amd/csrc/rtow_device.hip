@@ -588,21 +588,50 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
 // `r` in the medium's frame (a = dot(d, d)), called with the list's current
 // closest hit as tmax (hitableList.h:30): true and bt = the scatter distance
 // when the ray scatters inside.  Draws 1 or 2 numbers, as the reference.
-template <bool MEDIA, int STACK>
+// ANYB: media whose boundary needs the general traversal may occur (MB_ANY);
+// without them the kernel carries no nested traversal (fewer registers).
+template <bool MEDIA, int STACK, bool ANYB = true>
 __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
                          uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev);
 
-template <int STACK>
+template <int STACK, bool ANYB>
 __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, const Ray& wray,
                                            float tmin, float& bt, uint32_t* stk, int sp, Rng& rng, uint32_t& overflow) {
     const DMedium M = S.med[idx];
     (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
     float t1 = 0, t2 = 0;
-    bool two;
-    if ((M.boundary >> KIND_SHIFT) == DK_SPHERE) {
+    bool two = false;
+    if (M.bkind == MB_SPHERE) {
         const Sph s = load_sph(S.sph + (M.boundary & INDEX_MASK));
         two = S.unit_time ? sphere_boundary<true>(s, r, a, t1, t2) : sphere_boundary<false>(s, r, a, t1, t2);
-    } else {
+    } else if (M.bkind == MB_RECTS) {
+        // boundary->hit(-FLT_MAX, FLT_MAX) then boundary->hit(t1 + 0.0001,
+        // FLT_MAX) over instances of a Box: the nearest rectangle hit in each
+        // interval (hitableList.h:20-38 keeps the nearest; which rectangle
+        // does not matter here), in the rectangles' frame (chain bchain: the
+        // same transforms the traversal applies on the way down)
+        const Ray rb = chain_ray(S, M.bchain, wray);
+        const F3 inv = inv_dir(rb.d);
+        float lo = -FLT_MAX;
+        for (int pass = 0; pass < 2; pass++) {
+            float near = FLT_MAX, t;
+            bool f = false;
+            for (uint32_t k = 0; k < M.bcount; k++) {
+                if (rect_t(S.rect[M.bfirst + k], rb, inv, lo, near, t)) {
+                    near = t;
+                    f = true;
+                }
+            }
+            if (!f) break;
+            if (pass == 0) {
+                t1 = near;
+                lo = (float)((double)near + 0.0001);
+            } else {
+                t2 = near;
+                two = true;
+            }
+        }
+    } else if constexpr (ANYB) {
         Best b1, b2;
         two = traverse<false, STACK>(S, M.boundary, wray, M.chain, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow,
                                      mkref(DK_NONE, 0)) &&
@@ -636,7 +665,7 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
 // stk: this lane's LDS stack column.
 // `prev`: the leaf that holds tmax from before the call (DK_NONE: none), for
 // exact ties at tmax.
-template <bool MEDIA, int STACK>
+template <bool MEDIA, int STACK, bool ANYB>
 __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
                          uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev) {
     Ray r = chain_ray(S, chain0, wray);
@@ -734,7 +763,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             ra = 1.0f / a;
         } else if (kind == DK_MEDIUM) {
             if constexpr (MEDIA) {
-                if (medium_hit<STACK>(S, idx, r, a, wray, tmin, bt, stk, sp, rng, overflow)) {
+                if (medium_hit<STACK, ANYB>(S, idx, r, a, wray, tmin, bt, stk, sp, rng, overflow)) {
                     best.prim = cur;
                     found = true;
                 }
@@ -751,7 +780,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
 // The closest hit of a general scene whose root (below its instances) is a
 // list, scanned as hitableList.h:20-38 does: items in order, tmax the closest
 // hit so far.  The loop is uniform across the wave (see DTop).
-template <bool MEDIA, int STACK>
+template <bool MEDIA, int STACK, bool ANYB>
 __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
                              uint32_t& overflow) {
     float bt = FLT_MAX;
@@ -767,7 +796,7 @@ __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uin
         const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
         if (T.kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
             Best b;
-            if (traverse<MEDIA, STACK>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp)) {
+            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp)) {
                 bt = b.t;
                 bp = b.prim;
                 found = true;
@@ -1177,7 +1206,8 @@ __device__ __forceinline__ void shade_segment(const DevScene& S, const DevParams
 }
 
 // MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
-// chain), 2 general scene, 3 general scene with media
+// chain), 2 general scene, 3 general scene with media, 4 general scene with
+// media whose boundaries are spheres or Boxes (no nested general traversal)
 // All LDS is one dynamic region (16-B aligned carve, no static __shared__):
 // Perlin ranvec (4 KB) | perms (1 KB) | traversal stack STACK x BS words |
 // (LDSN) the DNode array of a simple scene.
@@ -1290,7 +1320,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         } else {
             Best best;
             best.prim = 0;
-            hit = traverse_top<MODE == 3, STACK>(S, ray, 0.001f, stk, rng, best, overflow);
+            hit = traverse_top<MODE >= 3, STACK, MODE == 3>(S, ray, 0.001f, stk, rng, best, overflow);
             if (hit) finalize<false>(S, best.prim, best.t, ray, rec);
         }
         if constexpr (DBG) {
@@ -1473,6 +1503,7 @@ struct HostLayout {
     uint32_t stack_need = 0;
     uint32_t chain_need = 0;
     bool has_media = false;
+    bool media_any = false;
     bool simple = false;
     bool unit_time = true;
     uint32_t root_chain_n = 0;
@@ -2522,6 +2553,33 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         L.stack_need = bd2.need(L.root, false).first;
     }
     if (!L.simple && tree == RTOW_TREE_SAH) buildTop(L);
+    // how each medium's boundary is queried (DMedium::bkind); REFERENCE mode
+    // keeps the general traversal for all of them
+    for (DMedium& M : L.med) {
+        M.bkind = MB_ANY;
+        if ((M.boundary >> KIND_SHIFT) == DK_SPHERE) {
+            M.bkind = MB_SPHERE;
+        } else if (tree == RTOW_TREE_SAH) {
+            uint32_t ref = M.boundary;
+            for (int guard = 0; guard < 64; guard++) {
+                const uint32_t k = ref >> KIND_SHIFT;
+                if (k != DK_TRANSLATE && k != DK_ROTY && k != DK_FLIP) break;
+                ref = L.inst[ref & INDEX_MASK].child;
+            }
+            if ((ref >> KIND_SHIFT) == DK_RECTS) {
+                const DList r = L.list[ref & INDEX_MASK];
+                bool one = r.count > 0;
+                for (uint32_t q = 1; q < r.count; q++) one = one && L.rect[r.first + q].chain == L.rect[r.first].chain;
+                if (one) {
+                    M.bkind = MB_RECTS;
+                    M.bfirst = r.first;
+                    M.bcount = r.count;
+                    M.bchain = L.rect[r.first].chain;
+                }
+            }
+        }
+        if (M.bkind == MB_ANY) L.media_any = true;
+    }
     if (L.sph_key.empty()) L.sph_key.push_back(0);
     if (L.rect_key.empty()) L.rect_key.push_back(0);
     if (L.med_key.empty()) L.med_key.push_back(0);
@@ -2632,9 +2690,11 @@ int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
                 return launchTrace<MODE, STACK, 4, false, 512, true>(c, cam, P, bpc, st);
         }
         if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
-        if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
         if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
-        if (c->waves == 2) return launchTrace<MODE, STACK, 2>(c, cam, P, bpc, st);
+        if constexpr (MODE != 4) {
+            if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
+            if (c->waves == 2) return launchTrace<MODE, STACK, 2>(c, cam, P, bpc, st);
+        }
     }
     return launchTrace<MODE, STACK, 1>(c, cam, P, bpc, st);
 }
@@ -2652,6 +2712,7 @@ int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32
     const DevScene& d = c->scene;
     if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
     if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
+    if (!d.media_any) return launchStack<4>(c, cam, P, bpc, st);
     return launchStack<3>(c, cam, P, bpc, st);
 }
 
@@ -2923,6 +2984,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.root = L.root;
     d.stack_need = L.stack_need;
     d.has_media = L.has_media ? 1u : 0u;
+    d.media_any = L.media_any ? 1u : 0u;
     d.simple = L.simple ? 1u : 0u;
     d.unit_time = L.unit_time ? 1u : 0u;
     d.root_chain_n = L.root_chain_n;

@@ -105,10 +105,16 @@ struct alignas(16) DList {  // 16 B: children at refs[first .. first+count)
     uint32_t first, count, pad0, pad1;
 };
 
-struct alignas(16) DMedium {  // 16 B, constantMedium.h:21-23
+// bkind: how the kernel queries the boundary (rtow_device.hip medium_hit):
+// MB_SPHERE a plain sphere (both roots from one quadratic), MB_RECTS instances
+// over a Box's rectangles rect[bfirst, +bcount) whose frame is chain bchain,
+// MB_ANY the general traversal.
+enum : uint32_t { MB_ANY = 0, MB_SPHERE = 1, MB_RECTS = 2 };
+struct alignas(16) DMedium {  // 32 B, constantMedium.h:21-23
     uint32_t boundary, phase_mat;
     float density;
     uint32_t chain;
+    uint32_t bkind, bfirst, bcount, bchain;
 };
 
 // The top-level list of a general scene (below the root's instances), as the
@@ -171,6 +177,7 @@ struct DevScene {
     uint32_t root;
     uint32_t stack_need;     // deepest traversal stack a ray can need
     uint32_t has_media;
+    uint32_t media_any;      // some medium's boundary needs the general traversal (MB_ANY)
     // "simple" worlds: a chain of instances at the root, then only BvhNodes
     // and spheres (the random scene) -- traversed by the BVH-only kernel
     uint32_t simple;
