@@ -218,7 +218,7 @@ __device__ __forceinline__ SlabRay slab_ray(const Ray& r) {
 
 // Conservative slab test for culling (never the reference's own AABB::hit,
 // whose divisions only decide WHICH subtrees it visits, not the result).
-// The box's exit is widened by |t|*1e-6 (> 2*gamma(3): rounding of the planes);
+// The box's exit is widened by 2^-19 relative (> 2*gamma(3): rounding of the planes);
 // tmax_c is the culling bound, the best hit so far widened by cull_bound().
 __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, float z0, float z1, const SlabRay& q,
                                      float tmin, float tmax_c, float& tnear) {
@@ -227,7 +227,9 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
     const float tz0 = (z0 - q.o.z) * q.inv.z, tz1 = (z1 - q.o.z) * q.inv.z;
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
     const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-    const float tf = fminf(ex + fabsf(ex) * 1.0e-6f, tmax_c);
+    // ex * (1 + 2^-19): for ex >= 0 the exit widened by 1.9e-6 relative; for
+    // ex < 0 the box lies behind the ray and stays culled (tn >= tmin > 0)
+    const float tf = fminf(ex * 1.0000019f, tmax_c);
     tnear = tn;
     return tn <= tf;
 }
@@ -471,6 +473,7 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
     uint32_t cur = root;
     uint32_t top = mkref(DK_NONE, 0);
     int sp = 0;
+    float btc = cull_bound(bt);  // follows bt: recomputed only when a sphere takes the record
     while (true) {
         if constexpr (PROF) {
             prof.lane_steps++;
@@ -506,22 +509,24 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
             float t;
             if (sph_closer(c, b0.w, r, a, ra, tmin, bt, best, refb, t)) {
                 bt = t;
+                btc = cull_bound(t);
                 best = refb;
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, cull_bound(bt), tb) && (refb >> KIND_SHIFT) == DK_BVH;
+            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
         }
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
             float t;
             if (sph_closer(c, a0.w, r, a, ra, tmin, bt, best, refa, t)) {
                 bt = t;
+                btc = cull_bound(t);
                 best = refa;
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, cull_bound(bt), ta) && (refa >> KIND_SHIFT) == DK_BVH;
+            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
         }
         // one back-edge, one exit: push / descend / pop are predicated updates
         const uint32_t NONE = mkref(DK_NONE, 0);
