@@ -17,8 +17,10 @@ Rank 0 prints ONE JSON line (value = whole-job Mray/s; Msample/s beside it).
 roofline.achieved = algorithmic bytes per launch (bytes/ray from the
 reference's own traversal counts, measured on the oracle at this scene and
 seed, times the launch's rays) / the trace kernel's mean duration from HIP
-events on the render stream.  cpu_baseline = the C oracle (a port of the
-reference loop) on the host cores over a bounded random pixel sample.
+events on the render stream.  cpu_baseline = the reference's own code
+(oracle/_ref/ref_harness) on the host cores over a bounded random pixel
+sample, rays counted by the C oracle on the same pixels (the oracle alone,
+kind "port", when the harness was not built).
 """
 import argparse
 import ctypes
@@ -51,14 +53,54 @@ def parse():
     ap.add_argument("--cpu-pixels", type=int, default=40000)
     ap.add_argument("--cpu-spp", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-kind", choices=["auto", "port"], default="auto",
+                    help="auto: the reference's own code when oracle/_ref was built, else the oracle")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_bench.json"))
     return ap.parse_args()
 
 
+def reference_run(pix, args, threads):
+    """The reference's own code (oracle/_ref/ref_harness, compiled from
+    /root/reference's headers in the build container; its render loop body is
+    main.cpp:938-951) on the same pixels: (seconds, checksum) or None when the
+    harness was not built.  The random scene loads its earth texture from
+    ./input_images/1_earth_8k.jpg (scenes.h:140): the synthetic texture the GPU
+    uses is staged there as a lossless PNG."""
+    import subprocess
+    import tempfile
+
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if not os.access(harness, os.X_OK):
+        return None
+    try:
+        from PIL import Image
+
+        import rtow
+    except ImportError:
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "input_images"))
+        Image.fromarray(rtow.synthetic_image(2048, 1024), "RGB").save(
+            os.path.join(d, "input_images", "1_earth_8k.jpg"), format="PNG")
+        pf = os.path.join(d, "pix.u32")
+        pix.tofile(pf)
+        env = dict(os.environ, RTOW_SCENE_SEED="1")
+        out = subprocess.run([harness, "bench", "random_ned", str(args.width), str(args.height), str(args.cpu_spp), pf,
+                              "--n", str(args.n), "--seed", str(args.seed), "--threads", str(threads), "--cwd", d],
+                             env=env, capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        return None
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    return r["seconds"], r["checksum"]
+
+
 def cpu_baseline(scene, cam, args, threads):
-    """Oracle (kind "port": the reference's render loop restated in C, bit-exact
-    with the reference build) on a bounded random pixel sample of the same
-    frame: returns the baseline dict and bytes/ray from its traversal counts."""
+    """The CPU render of a bounded random pixel sample of the same frame: the
+    reference's own code (kind "reference", oracle/_ref) when it was built, the
+    oracle otherwise (kind "port": the reference's render loop restated in C,
+    bit-exact with the reference build).  The oracle always runs: its traversal
+    counts give the ray count (the same paths: the two agree bit for bit, and
+    the checksum of the pixel sums shows it) and bytes/ray."""
     import scene_io as sio
 
     rng = np.random.default_rng(1234)
@@ -67,14 +109,24 @@ def cpu_baseline(scene, cam, args, threads):
     ocam = sio.RtowCamera.from_buffer_copy(bytes(cam))
     p = sio.default_params(W, H, args.cpu_spp, seed=args.seed)
     t0 = time.perf_counter()
-    _, _, c = sio.oracle_render(scene.view_ptr, ocam, p, pixels=pix, threads=threads)
+    lin, _, c = sio.oracle_render(scene.view_ptr, ocam, p, pixels=pix, threads=threads)
     dt = time.perf_counter() - t0
     bytes_per_ray = (c.bvh_visits * BYTES_BVH + c.sphere_tests * BYTES_SPHERE + c.moving_sphere_tests * BYTES_MSPHERE
                      + c.rect_tests * BYTES_RECT + c.medium_calls * BYTES_MEDIUM) / max(c.segments, 1)
-    base = {"value": round(c.segments / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+    sample = f"{len(pix)} random pixels of the {W}x{H} frame x {args.cpu_spp} spp (same scene/seed), {threads} threads"
+    port = {"value": round(c.segments / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
             "msample_per_s": round(c.samples / dt / 1e6, 4), "seconds": round(dt, 2),
-            "sample": f"{len(pix)} random pixels of the {W}x{H} frame x {args.cpu_spp} spp (same scene/seed), "
-                      f"oracle/librtow_oracle.so, {threads} threads"}
+            "sample": sample + ", oracle/librtow_oracle.so"}
+    base = port
+    ref = reference_run(pix, args, threads) if args.cpu_kind != "port" else None
+    if ref is not None:
+        rs, checksum = ref
+        osum = float(lin.astype(np.float64).sum())
+        base = {"value": round(c.segments / rs / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "reference",
+                "msample_per_s": round(c.samples / rs / 1e6, 4), "seconds": round(rs, 2),
+                "sample": sample + ", oracle/_ref/ref_harness (the reference's headers); rays counted by the oracle",
+                "same_result_as_oracle": bool(abs(checksum - osum) <= 1e-6 * max(1.0, abs(osum))),
+                "port": {k: port[k] for k in ("value", "msample_per_s", "seconds")}}
     counts = {"segments_per_sample": c.segments / max(c.samples, 1),
               "bvh_visits_per_ray": c.bvh_visits / max(c.segments, 1),
               "sphere_tests_per_ray": c.sphere_tests / max(c.segments, 1),

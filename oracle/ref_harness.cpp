@@ -22,6 +22,7 @@
 //   ref_harness camera <W> <H> <out.cam>
 //   ref_harness camera_oriented <W> <H> <lookfrom xyz> <view xyz> <east xyz> <down xyz> <out.cam>
 //   ref_harness render <scene> <W> <H> <spp> <out_prefix> [opts]
+//   ref_harness bench  <scene> <W> <H> <spp> <pixels.u32> [opts]   (timing, JSON line)
 //       writes <out_prefix>.lin (W*H*3 float32, framebuffer order) and
 //       <out_prefix>.bgra (W*H*4 bytes, main.cpp:982-989)
 // scenes: three_sphere | random_ned | cornell | cornell_smoke | final_ned
@@ -32,6 +33,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -508,6 +510,31 @@ static void renderWorker(int id, int nthreads, Camera* cam, Hitable* world, uint
     }
 }
 
+// `bench`: the same loop body over a list of framebuffer pixels (x + W*y,
+// top-down, as the oracle's rtow_oracle_render_pixels takes them), T threads
+// interleaving the list -- the reference's own code timed on a bounded
+// sample of a frame (bench.py's cpu_baseline, kind "reference").
+static void benchWorker(int id, int nthreads, Camera* cam, Hitable* world, uint32_t W, uint32_t H, uint32_t spp,
+                        uint64_t seed, const std::vector<uint32_t>* pix, double* sum) {
+    double acc = 0.0;
+    for (size_t i = (size_t)id; i < pix->size(); i += (size_t)nthreads) {
+        const uint32_t fb = (*pix)[i];
+        const int column = (int)(fb % W), row = (int)(H - 1 - fb / W);
+        vec3 outputColor(0, 0, 0);
+        for (uint32_t sample = 0; sample < spp; sample++) {
+            CbEngine::key = rtow_sample_key(seed, (uint32_t)row * W + (uint32_t)column, sample);
+            CbEngine::ctr = 0;
+            float u = (float)(column + unifRand(randomNumberGenerator)) / (float)W;
+            float v = (float)(row + unifRand(randomNumberGenerator)) / (float)H;
+            ray rayCast = cam->getRay(u, v);
+            outputColor += color(rayCast, world, 0);
+        }
+        outputColor /= float(spp);
+        acc += (double)outputColor[0] + (double)outputColor[1] + (double)outputColor[2];
+    }
+    *sum = acc;
+}
+
 static Opts parseOpts(int argc, char** argv, int first) {
     Opts o;
     for (int k = first; k < argc; k++) {
@@ -581,6 +608,35 @@ int main(int argc, char** argv) {
         f = std::fopen((prefix + ".bgra").c_str(), "wb");
         std::fwrite(bgra.data(), 1, bgra.size(), f);
         std::fclose(f);
+        return 0;
+    }
+    if (cmd == "bench" && argc >= 7) {
+        Opts o = parseOpts(argc, argv, 7);
+        uint32_t W = (uint32_t)std::atoi(argv[3]), H = (uint32_t)std::atoi(argv[4]);
+        uint32_t spp = (uint32_t)std::atoi(argv[5]);
+        std::vector<uint32_t> pix;
+        {
+            FILE* f = std::fopen(argv[6], "rb");
+            if (!f) { std::perror("pixels"); return 2; }
+            uint32_t v;
+            while (std::fread(&v, 4, 1, f) == 1)
+                if (v < W * H) pix.push_back(v);
+            std::fclose(f);
+        }
+        Hitable* world = buildWorld(argv[2], o);
+        Camera* cam = mainCamera(W, H);
+        int nt = o.threads > 0 ? o.threads : (int)std::thread::hardware_concurrency();
+        std::vector<double> sums((size_t)nt, 0.0);
+        std::vector<std::thread> ts;
+        auto t0 = std::chrono::steady_clock::now();
+        for (int t = 0; t < nt; t++)
+            ts.emplace_back(benchWorker, t, nt, cam, world, W, H, spp, o.seed, &pix, &sums[(size_t)t]);
+        for (auto& t : ts) t.join();
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        double sum = 0.0;
+        for (double x : sums) sum += x;
+        std::printf("{\"seconds\": %.6f, \"pixels\": %zu, \"samples\": %llu, \"threads\": %d, \"checksum\": %.9g}\n",
+                    sec, pix.size(), (unsigned long long)pix.size() * spp, nt, sum);
         return 0;
     }
     std::fprintf(stderr, "bad command\n");
