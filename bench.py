@@ -202,8 +202,13 @@ def main():
         threads = min(16, os.cpu_count() or 1)
         if args.no_cpu:
             base, bpr, counts = None, None, {}
-        else:
+        elif world == 1:
             base, bpr, counts = cpu_baseline(scene, cam, args, threads)
+        else:  # the CPU baseline is quoted at N=1 only; bytes/ray from a smaller oracle sample
+            args.cpu_pixels = max(1, args.cpu_pixels // 10)
+            args.cpu_kind = "port"
+            _, bpr, counts = cpu_baseline(scene, cam, args, threads)
+            base = None
         mean_kms = float(np.mean(kms))
         launch_rays = segs / max(args.steps, 1)
         roof = None
