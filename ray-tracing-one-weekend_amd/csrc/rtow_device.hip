@@ -851,12 +851,21 @@ __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uin
     return found;
 }
 
+// x / d in double from r = RN(1/d): q0 = x*r, one fma residual step.  For the
+// two divisions below it equals the IEEE quotient for every float phi in
+// [-pi, pi] and theta in [-pi/2, pi/2] (all 4.3e9 checked on the host;
+// tests/test_numerics.py samples them), at 3 f64 ops instead of ~10.
+__device__ __forceinline__ double div_by_f64(double x, double d, double r) {
+    const double q0 = x * r;
+    return fma(fma(-q0, d, x), r, q0);
+}
+
 // mathUtilities.h:62-68
 __device__ __forceinline__ void sphere_uv(F3 p, float& u, float& v) {
     const float phi = atan2f(p.z, p.x);
     const float theta = asinf(p.y);
-    u = (float)(1 - (phi + M_PI) / (2 * M_PI));
-    v = (float)((theta + M_PI / 2) / M_PI);
+    u = (float)(1 - div_by_f64(phi + M_PI, 2 * M_PI, 1.0 / (2 * M_PI)));
+    v = (float)div_by_f64(theta + M_PI / 2, M_PI, 1.0 / M_PI);
 }
 
 // The HitRecord of the winning leaf: the ray into the leaf's frame (its
@@ -1020,7 +1029,11 @@ __device__ F3 leaf_tex_value(const DevScene& S, uint32_t ti, float u, float v, F
         if (i > nx - 1) i = nx - 1;
         if (j > ny - 1) j = ny - 1;
         const size_t o = 3 * (size_t)i + 3 * (size_t)nx * (size_t)j;
-        return f3((float)(data[o] / 255.0), (float)(data[o + 1] / 255.0), (float)(data[o + 2] / 255.0));
+        // (float)(c / 255.0) == div_by((float)c, 255, RN(1/255)) for all 256 c
+        // (tests/test_numerics.py): float ops instead of three f64 divisions
+        const float r255 = 1.0f / 255.0f;
+        return f3(div_by((float)data[o], 255.0f, r255), div_by((float)data[o + 1], 255.0f, r255),
+                  div_by((float)data[o + 2], 255.0f, r255));
     }
     return f3(0, 0, 0);
 }

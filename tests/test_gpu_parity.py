@@ -139,6 +139,15 @@ def test_scene_reupload_and_bad_params(gpu_ctx):
         gpu_ctx.render(cam, rtow.params(0, 8, 1))
     with pytest.raises(rtow.RtowError):
         gpu_ctx.render_tiles_device(cam, rtow.params(16, 8, 1, rank=3, world=2), 0)
+    with pytest.raises(rtow.RtowError):  # spp 0
+        gpu_ctx.render(cam, rtow.params(16, 8, 0))
+    with pytest.raises(rtow.RtowError):  # wider than 2^24 (float pixel coordinates stop being exact)
+        gpu_ctx.render_tiles_device(cam, rtow.params((1 << 24) + 8, 1, 1), 0)
+    with pytest.raises(rtow.RtowError):  # more than 2^31 pixels
+        gpu_ctx.render_tiles_device(cam, rtow.params(1 << 16, (1 << 15) + 8, 1), 0)
+    # the context still renders after the refusals
+    bgra, _, st = gpu_ctx.render(cam, rtow.params(16, 8, 2), linear=False)
+    assert st.samples == 16 * 8 * 2 and bgra.size == 16 * 8 * 4
 
 
 def test_full_frame_every_pixel_against_oracle(gpu_ctx):

@@ -47,3 +47,45 @@ def test_fma_corrected_division_is_the_ieee_quotient(tmp_path):
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
     bad, n = map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split())
     assert n > 40_000_000 and bad == 0
+
+
+SRC_F64 = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+static inline double mk(double x, double d, double r) { double q0 = x * r; return fma(fma(-q0, d, x), r, q0); }
+int main(int argc, char** argv) {
+    const long step = 97;  /* the device claim was checked for every float; this samples them */
+    const double d1 = 2 * M_PI, r1 = 1.0 / d1, d2 = M_PI, r2 = 1.0 / d2;
+    long bad = 0, n = 0;
+    for (long u = 0; u < (1L << 32); u += step) {
+        float f; uint32_t b = (uint32_t)u; memcpy(&f, &b, 4);
+        if (f >= -3.14159274f && f <= 3.14159274f) { double x = (double)f + M_PI; bad += x / d1 != mk(x, d1, r1); n++; }
+        if (f >= -1.57079637f && f <= 1.57079637f) { double x = (double)f + M_PI / 2; bad += x / d2 != mk(x, d2, r2); n++; }
+    }
+    const float r = 1.0f / 255.0f;
+    for (int i = 0; i < 256; i++) {
+        float x = (float)i, q0 = x * r, q = fmaf(fmaf(-q0, 255.0f, x), r, q0);
+        bad += q != (float)(i / 255.0); n++;
+    }
+    printf("%ld %ld\n", bad, n);
+    return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_uv_and_texel_divisions(tmp_path):
+    """sphere_uv's (phi + pi) / 2pi and (theta + pi/2) / pi (mathUtilities.h:
+    62-68) in double via the reciprocal and one fma residual step equal the
+    IEEE quotients for the floats atan2f / asinf return (every one of the
+    4.3e9 was checked once; this samples every 97th bit pattern), and
+    ImageTexture's c / 255.0 (texture.h:76), rounded to float, is div_by's
+    float result for all 256 byte values."""
+    src = tmp_path / "f64.c"
+    src.write_text(SRC_F64)
+    exe = tmp_path / "f64"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"], check=True)
+    bad, n = (int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split())
+    assert n > 40_000_000 and bad == 0

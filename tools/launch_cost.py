@@ -23,7 +23,7 @@ km, tm = [], []
 for spp in spps:
     ks, ts = [], []
     for _ in range(3):
-        st = ctx.render_tiles_device(cam, rtow.params(W, H, spp, seed=1), slab.data_ptr())
+        st = ctx.render_tiles_device(cam, rtow.params(W, H, spp, seed=1, max_depth=int(os.environ.get("LC_DEPTH", "50"))), slab.data_ptr())
         ks.append(st.kernel_ms)
         ts.append(st.total_ms)
     km.append(min(ks))
