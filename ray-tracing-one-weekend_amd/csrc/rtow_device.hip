@@ -373,6 +373,55 @@ __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, const F3& i
     return true;
 }
 
+// AABB::hit (aabb.h:22-43) exactly: true divisions, ffmin/ffmax, `tmax <= tmin`
+// (a NaN comparison does not reject).  b: min xyz, 0, max xyz, 0.
+__device__ __forceinline__ bool ref_slab(float mn, float mx, float o, float d, float& tmin, float& tmax) {
+    const float p = (mn - o) / d, q = (mx - o) / d;
+    const float t0 = p < q ? p : q, t1 = p > q ? p : q;
+    tmin = t0 > tmin ? t0 : tmin;
+    tmax = t1 < tmax ? t1 : tmax;
+    return !(tmax <= tmin);
+}
+__device__ __forceinline__ bool ref_aabb_hit(const float* b, const Ray& r, float tmin, float tmax) {
+    const float4 lo = *(const float4*)b, hi = *(const float4*)(b + 4);
+    return ref_slab(lo.x, hi.x, r.o.x, r.d.x, tmin, tmax) && ref_slab(lo.y, hi.y, r.o.y, r.d.y, tmin, tmax) &&
+           ref_slab(lo.z, hi.z, r.o.z, r.d.z, tmin, tmax);
+}
+
+// Does the reference test rectangle `rect` for this ray at all?  BvhNode::hit
+// (bvhNode.h:66-71) tests its own box before its children, with the interval
+// color() hands down (tmin, MAXFLOAT), so a ray that grazes a box edge -- one
+// point or an empty interval after rounding -- never reaches the Box's sides
+// there, although the rectangle test (closed bounds) would take the edge
+// point.  `r`: the ray in the rectangle's frame, which is the frame of the
+// BvhNodes recorded for it.
+__device__ __forceinline__ bool ref_reaches_rect(const DevScene& S, uint32_t rect, const Ray& r, float tmin) {
+    const uint32_t a = S.rect_anc[rect];
+    const uint32_t n = a & 255u, off = a >> 8;
+    for (uint32_t k = 0; k < n; k++)
+        if (!ref_aabb_hit(S.abox + 8 * (size_t)(off + k), r, tmin, FLT_MAX)) return false;
+    return true;
+}
+
+// The winning hit of a traversal, rectangle `rect` at t: would the reference
+// have skipped it (ref_reaches_rect)?  Only a hit within rounding of the
+// rectangle's edge can be skipped (a ray through a face's interior crosses
+// its box, and every box above it, in an interval of positive length), so the
+// box tests run only for hits within 2^-14 (relative to the rectangle's
+// coordinates) of an edge.  `wray`: the world ray.
+__device__ __forceinline__ bool ref_skips_hit(const DevScene& S, uint32_t rect, const Ray& wray, float t, float tmin) {
+    if ((S.rect_anc[rect] & 255u) == 0) return false;
+    const DRect q = S.rect[rect];
+    const Ray r = chain_ray(S, q.chain, wray);
+    uint32_t i, j, k;
+    rect_axes(q.axis & 3u, i, j, k);
+    const float x = comp(r.o, i) + t * comp(r.d, i);
+    const float y = comp(r.o, j) + t * comp(r.d, j);
+    const float ex = (fabsf(q.a0) + fabsf(q.a1) + 1.0f) * 0x1p-14f, ey = (fabsf(q.b0) + fabsf(q.b1) + 1.0f) * 0x1p-14f;
+    const bool edge = x - q.a0 < ex || q.a1 - x < ex || y - q.b0 < ey || q.b1 - y < ey;
+    return edge && !ref_reaches_rect(S, rect, r, tmin);
+}
+
 // Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
 struct Prof {
     uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
@@ -603,7 +652,8 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
 // without them the kernel carries no nested traversal (fewer registers).
 template <bool MEDIA, int STACK, bool ANYB = true>
 __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
-                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev);
+                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev,
+                         bool strict = false);
 
 template <int STACK, bool ANYB>
 __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, const Ray& wray,
@@ -678,7 +728,8 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
 // exact ties at tmax.
 template <bool MEDIA, int STACK, bool ANYB>
 __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
-                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev) {
+                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev,
+                         bool strict) {
     Ray r = chain_ray(S, chain0, wray);
     SlabRay q = slab_ray(r);
     float a = dot(r.d, r.d);
@@ -717,8 +768,8 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             }
         } else if (kind == DK_RECT) {
             float t;
-            if (rect_t(S.rect[idx], r, q.inv, tmin, bt, t) &&
-                (t < bt || wins_tie(S, cur, best.prim))) {
+            if (rect_t(S.rect[idx], r, q.inv, tmin, bt, t) && (t < bt || wins_tie(S, cur, best.prim)) &&
+                (!strict || ref_reaches_rect(S, idx, r, tmin))) {
                 bt = t;
                 best.prim = cur;
                 found = true;
@@ -729,8 +780,8 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
             for (uint32_t j = 0; j < R.count; j++) {
                 const uint32_t ref = mkref(DK_RECT, R.first + j);
                 float t;
-                if (rect_t(S.rect[R.first + j], r, q.inv, tmin, bt, t) &&
-                    (t < bt || wins_tie(S, ref, best.prim))) {
+                if (rect_t(S.rect[R.first + j], r, q.inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, best.prim)) &&
+                    (!strict || ref_reaches_rect(S, R.first + j, r, tmin))) {
                     bt = t;
                     best.prim = ref;
                     found = true;
@@ -793,7 +844,7 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
 // hit so far.  The loop is uniform across the wave (see DTop).
 template <bool MEDIA, int STACK, bool ANYB>
 __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
-                             uint32_t& overflow) {
+                             uint32_t& overflow, bool strict) {
     float bt = FLT_MAX;
     uint32_t bp = mkref(DK_NONE, 0);
     bool found = false;
@@ -807,7 +858,7 @@ __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uin
         const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
         if (T.kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
             Best b;
-            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp)) {
+            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp, strict)) {
                 bt = b.t;
                 bp = b.prim;
                 found = true;
@@ -1344,7 +1395,21 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         } else {
             Best best;
             best.prim = 0;
-            hit = traverse_top<MODE >= 3, STACK, MODE == 3>(S, ray, 0.001f, stk, rng, best, overflow);
+            // a winning rectangle the reference would not have reached (its
+            // boxes grazed at an edge): trace the ray again, this time testing
+            // every rectangle hit against the reference's boxes (same draws)
+            const Rng rng0 = rng;
+            bool strict = false;
+            while (true) {
+                hit = traverse_top<MODE >= 3, STACK, MODE == 3>(S, ray, 0.001f, stk, rng, best, overflow, strict);
+                if (!strict && hit && (best.prim >> KIND_SHIFT) == DK_RECT &&
+                    ref_skips_hit(S, best.prim & INDEX_MASK, ray, best.t, 0.001f)) {
+                    rng = rng0;
+                    strict = true;
+                    continue;
+                }
+                break;
+            }
             if (hit) finalize<false>(S, best.prim, best.t, ray, rec);
         }
         if constexpr (DBG) {
@@ -1536,6 +1601,9 @@ struct HostLayout {
     std::vector<unsigned long long> sph_key, rect_key, med_key;
     std::vector<DChain> chains;
     std::vector<DTop> top;
+    std::vector<float> bvh_own;      // 6 per reference BvhNode slot: its own box (bvhNode.h:58)
+    std::vector<uint32_t> rect_anc;  // DevScene::rect_anc
+    std::vector<float> abox;         // DevScene::abox
 };
 
 // ---------------------------------------------------------------------------
@@ -2310,6 +2378,8 @@ struct Converter {
             }
             uint32_t slot = (uint32_t)L.bvh.size();
             L.bvh.push_back(DBvh{});
+            L.bvh_own.resize(L.bvh.size() * 6, 0.0f);
+            for (int q = 0; q < 6; q++) L.bvh_own[6 * (size_t)slot + q] = h.f[q];
             ref = mkref(DK_BVH, slot);
             memo[hi] = ref;
             uint32_t l = conv(h.a, true), r = conv(h.b, true);
@@ -2396,6 +2466,55 @@ struct Bounds {
         return r;
     }
 };
+
+// For every rectangle, the own boxes of the reference BvhNodes above it in
+// its frame (DevScene::rect_anc / abox; ref_reaches_rect).  A Translate or
+// RotateY starts a new frame (boxes above it see another ray: dropped, so
+// those are not checked); FlipNormals keeps the ray.  Medium boundaries are
+// queried with (-FLT_MAX, FLT_MAX) and sit below no BvhNode: not recorded.
+void refAncestors(HostLayout& L, uint32_t ref, std::vector<uint32_t>& path, int depth = 0) {
+    if (depth > 4096) return;
+    const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+    auto record = [&](uint32_t rect) {
+        if (path.empty() || path.size() > 255 || rect >= L.rect_anc.size()) return;
+        const uint32_t off = (uint32_t)(L.abox.size() / 8);
+        if (off >= (1u << 24)) return;
+        for (uint32_t b : path) {
+            const float* o = &L.bvh_own[6 * (size_t)b];
+            const float box[8] = {o[0], o[1], o[2], 0.0f, o[3], o[4], o[5], 0.0f};
+            L.abox.insert(L.abox.end(), box, box + 8);
+        }
+        L.rect_anc[rect] = (off << 8) | (uint32_t)path.size();
+    };
+    switch (kind) {
+    case DK_BVH:
+        path.push_back(idx);
+        refAncestors(L, L.bvh[idx].left, path, depth + 1);
+        refAncestors(L, L.bvh[idx].right, path, depth + 1);
+        path.pop_back();
+        break;
+    case DK_LIST:
+        for (uint32_t j = 0; j < L.list[idx].count; j++) refAncestors(L, L.refs[L.list[idx].first + j], path, depth + 1);
+        break;
+    case DK_RECTS:
+        for (uint32_t j = 0; j < L.list[idx].count; j++) record(L.list[idx].first + j);
+        break;
+    case DK_RECT:
+        record(idx);
+        break;
+    case DK_FLIP:
+        refAncestors(L, L.inst[idx].child, path, depth + 1);
+        break;
+    case DK_TRANSLATE:
+    case DK_ROTY: {
+        std::vector<uint32_t> fresh;
+        refAncestors(L, L.inst[idx].child, fresh, depth + 1);
+        break;
+    }
+    default:
+        break;
+    }
+}
 
 // DTop descriptors of a general scene whose root, below its instances, is a
 // list (empty otherwise)
@@ -2569,6 +2688,11 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     {
         std::vector<KeyComp> path;
         assignTieKeys(L, L.root, path);
+    }
+    L.rect_anc.assign(L.rect.size(), 0u);
+    if (!L.simple) {  // the reference BvhNodes above each rectangle (before the trees are rebuilt)
+        std::vector<uint32_t> path;
+        refAncestors(L, L.root, path);
     }
     if (!L.simple && tree == RTOW_TREE_SAH) {  // after the tie keys: they come from the reference trees
         GeneralSah g{L, (uint32_t)L.bvh.size()};
@@ -2974,6 +3098,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     std::vector<DTop> top = L.top;
     if (top.empty()) top.push_back(DTop{});
     size_t o_top = pushBlob(blob, top);
+    if (L.rect_anc.empty()) L.rect_anc.push_back(0u);
+    if (L.abox.empty()) L.abox.assign(8, 0.0f);
+    size_t o_anc = pushBlob(blob, L.rect_anc), o_abox = pushBlob(blob, L.abox);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -3005,6 +3132,8 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.med_key = (const unsigned long long*)(b + o_km);
     d.top = (const DTop*)(b + o_top);
     d.n_top = (uint32_t)L.top.size();
+    d.rect_anc = (const uint32_t*)(b + o_anc);
+    d.abox = (const float*)(b + o_abox);
     d.root = L.root;
     d.stack_need = L.stack_need;
     d.has_media = L.has_media ? 1u : 0u;

@@ -162,6 +162,12 @@ struct DevScene {
     const DChain* chains;
     const DTop* top;         // general scenes: the top-level list, n_top items (0: none)
     uint32_t n_top;
+    // Per rectangle: (offset << 8) | count of the boxes (8 floats each in
+    // abox: min xyz, 0, max xyz, 0) of the reference BvhNodes above it in its
+    // own frame -- the boxes the reference's AABB::hit tests before it tests
+    // the rectangle at all (see ref_reaches_rect).
+    const uint32_t* rect_anc;
+    const float* abox;
     // Tie keys (general scenes): per sphere / rectangle / medium leaf, the
     // order in which the reference settles an exact tie in t (see
     // assignTieKeys in rtow_device.hip): the larger key wins.

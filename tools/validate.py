@@ -4,7 +4,7 @@ bit-exact to the reference): each config at its full resolution (config 5 at
 config (per-channel RMS of the linear frame, max |diff|, pixels off by more
 than 1e-3, share of bit-identical channel values, segment counts).
 
-  python tools/validate.py [--out FILE]
+  python tools/validate.py [--out FILE] [--scenes a,b]
 """
 import argparse
 import json
@@ -26,6 +26,7 @@ CASES = [("three_sphere", 0, 200, 100, 8), ("random_ned", 487, 1920, 1080, 16), 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
+    ap.add_argument("--scenes", default=None, help="comma-separated subset of the configs")
     args = ap.parse_args()
     import torch
 
@@ -33,7 +34,8 @@ def main():
     threads = min(16, os.cpu_count() or 1)
     ctx = rtow.Context(0)
     lines = []
-    for name, n, W, H, spp in CASES:
+    cases = [c for c in CASES if args.scenes is None or c[0] in args.scenes.split(",")]
+    for name, n, W, H, spp in cases:
         scene = rtow.Scene.build(name, n=max(n, 1), image="synthetic", scene_seed=1)
         ctx.upload(scene)
         cam = rtow.camera_main(W, H)
