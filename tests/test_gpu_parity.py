@@ -229,3 +229,31 @@ def test_long_flat_list_matches_oracle(gpu_ctx):
         olin, _, _ = sio.oracle_render(sc.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
                                        sio.RtowParams.from_buffer_copy(bytes(p)))
         assert (channel_rms(lin, olin) <= RMS_TOL).all(), scene
+
+
+# (x, y, sample) of final_ned 1024x1024x16, seed 7, whose paths graze a ground
+# box's edge, where the reference's AABB::hit (aabb.h:22-43) never tests the
+# Box's sides; found with tools/find_grazing.py (the build before the fix
+# traced all four differently from the oracle)
+GRAZING = [(399, 642, 10), (998, 664, 6), (669, 774, 1), (911, 784, 3)]
+
+
+@pytest.mark.parametrize("tree", ["sah", "reference"])
+def test_grazing_box_edges_follow_the_reference(tree):
+    W, H, spp = 1024, 1024, 16
+    ctx = rtow.Context(0)
+    try:
+        ctx.set_tree(tree)
+        sc = rtow.Scene.build("final_ned", n=1, image="synthetic", scene_seed=1)
+        ctx.upload(sc)
+        cam = rtow.camera_main(W, H)
+        p = rtow.params(W, H, spp, seed=7)
+        ocam = sio.RtowCamera.from_buffer_copy(bytes(cam))
+        op = sio.RtowParams.from_buffer_copy(bytes(p))
+        for x, y, s in GRAZING:
+            g = ctx.trace_sample(cam, p, x, y, s)
+            o = sio.oracle_trace(sc.view_ptr, ocam, op, x, y, s)
+            assert len(g) == len(o), (x, y, s)
+            assert np.array_equal(g[:, :11], o[:, :11]), (x, y, s)
+    finally:
+        ctx.close()
