@@ -1602,6 +1602,10 @@ struct HostLayout {
     std::vector<DChain> chains;
     std::vector<DTop> top;
     std::vector<float> bvh_own;      // 6 per reference BvhNode slot: its own box (bvhNode.h:58)
+    // n == 1 BvhNodes (collapsed into their leaf): the leaf's ref -> index of
+    // the node's own box (6 floats) in collapsed_own; AABB::hit still tests it
+    std::vector<float> collapsed_own;
+    std::unordered_map<uint32_t, uint32_t> collapsed_of;
     std::vector<uint32_t> rect_anc;  // DevScene::rect_anc
     std::vector<float> abox;         // DevScene::abox
 };
@@ -2374,6 +2378,8 @@ struct Converter {
         case RTOW_HIT_BVH_NODE: {
             if (h.a == h.b) {  // n == 1 node: both children are the same leaf
                 ref = conv(h.a, true);
+                L.collapsed_of[ref] = (uint32_t)(L.collapsed_own.size() / 6);
+                L.collapsed_own.insert(L.collapsed_own.end(), h.f, h.f + 6);
                 break;
             }
             uint32_t slot = (uint32_t)L.bvh.size();
@@ -2468,19 +2474,31 @@ struct Bounds {
 };
 
 // For every rectangle, the own boxes of the reference BvhNodes above it in
-// its frame (DevScene::rect_anc / abox; ref_reaches_rect).  A Translate or
-// RotateY starts a new frame (boxes above it see another ray: dropped, so
+// its frame (DevScene::rect_anc / abox; ref_reaches_rect), n == 1 nodes
+// included (collapsed into their leaf here, still tested by AABB::hit there:
+// a ray through the edge two adjacent Boxes share grazes such a node's box,
+// which is the Box's own).  A Translate or RotateY starts a new frame (boxes above it see another ray: dropped, so
 // those are not checked); FlipNormals keeps the ray.  Medium boundaries are
 // queried with (-FLT_MAX, FLT_MAX) and sit below no BvhNode: not recorded.
 void refAncestors(HostLayout& L, uint32_t ref, std::vector<uint32_t>& path, int depth = 0) {
     if (depth > 4096) return;
     const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+    // path entries: a BvhNode slot, or (bit 31) a collapsed n == 1 node's box
+    const auto col = L.collapsed_of.find(ref);
+    const bool collapsed = col != L.collapsed_of.end();
+    if (collapsed) path.push_back(0x80000000u | col->second);
     auto record = [&](uint32_t rect) {
         if (path.empty() || path.size() > 255 || rect >= L.rect_anc.size()) return;
         const uint32_t off = (uint32_t)(L.abox.size() / 8);
         if (off >= (1u << 24)) return;
         for (uint32_t b : path) {
-            const float* o = &L.bvh_own[6 * (size_t)b];
+            const bool c = (b & 0x80000000u) != 0;
+            const size_t at = 6 * (size_t)(b & 0x7fffffffu);
+            if (at + 6 > (c ? L.collapsed_own.size() : L.bvh_own.size())) return;  // (not a reference node)
+        }
+        for (uint32_t b : path) {
+            const float* o = (b & 0x80000000u) ? &L.collapsed_own[6 * (size_t)(b & 0x7fffffffu)]
+                                               : &L.bvh_own[6 * (size_t)b];
             const float box[8] = {o[0], o[1], o[2], 0.0f, o[3], o[4], o[5], 0.0f};
             L.abox.insert(L.abox.end(), box, box + 8);
         }
@@ -2514,6 +2532,7 @@ void refAncestors(HostLayout& L, uint32_t ref, std::vector<uint32_t>& path, int 
     default:
         break;
     }
+    if (collapsed) path.pop_back();
 }
 
 // DTop descriptors of a general scene whose root, below its instances, is a

@@ -235,7 +235,8 @@ def test_long_flat_list_matches_oracle(gpu_ctx):
 # box's edge, where the reference's AABB::hit (aabb.h:22-43) never tests the
 # Box's sides; found with tools/find_grazing.py (the build before the fix
 # traced all four differently from the oracle)
-GRAZING = [(399, 642, 10), (998, 664, 6), (669, 774, 1), (911, 784, 3)]
+GRAZING = [(399, 642, 10), (998, 664, 6), (669, 774, 1), (911, 784, 3),
+           (979, 734, 6)]  # through the edge two ground boxes share: an n == 1 BvhNode's box
 
 
 @pytest.mark.parametrize("tree", ["sah", "reference"])
