@@ -14,13 +14,23 @@ the fixed frame, so scaling is "strong".
       --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line (value = whole-job Mray/s; Msample/s beside it).
-roofline.achieved = algorithmic bytes per launch (bytes/ray from the
-reference's own traversal counts, measured on the oracle at this scene and
-seed, times the launch's rays) / the trace kernel's mean duration from HIP
-events on the render stream.  cpu_baseline = the reference's own code
-(oracle/_ref/ref_harness) on the host cores over a bounded random pixel
-sample, rays counted by the C oracle on the same pixels (the oracle alone,
-kind "port", when the harness was not built).
+
+roofline: the bound that limits this kernel is VALU issue, not HBM (the scene
+is LDS/L2-resident; measured HBM traffic is ~7 GB/s).  achieved = VALU
+wave-instructions per second of the trace kernel = (wave-instructions per ray,
+SQ_INSTS_VALU from the committed rocprofv3 PMC pass of this exact build and
+config, profiles/<round>_*/pmc_summary.json) x the rays this launch traced /
+the kernel's mean duration from HIP events on the render stream.  peak = 1024
+SIMDs x 2.4 GHz x 0.5 (a wave64 VALU instruction occupies a SIMD-32 for two
+cycles, MI355X_MICROARCH.md).  lane_util = the active-lane fraction of those
+instructions (SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64), calibrated on
+gfx950 by tools/valu_calib.hip), so frac x lane_util is the useful-lane share
+of the chip's VALU throughput.  The measured HBM bytes (FETCH_SIZE x 2 +
+WRITE_SIZE of the same PMC run) and the reference-equivalent record bytes per
+ray are informational fields.  cpu_baseline = the reference's
+own code (oracle/_ref/ref_harness) on all the host cores this process may use
+over a bounded random pixel sample, rays counted by the C oracle on the same
+pixels (the oracle alone, kind "port", when the harness was not built).
 """
 import argparse
 import ctypes
@@ -36,6 +46,10 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMD-32, a wave64 VALU instruction takes two
+# cycles of its SIMD, 2.4 GHz max clock (MI355X_MICROARCH.md) -> G wave-instr/s
+N_SIMD, CLOCK_GHZ = 1024, 2.4
+VALU_PEAK_G = N_SIMD * CLOCK_GHZ * 0.5
 # algorithmic record bytes per reference traversal event
 BYTES_BVH, BYTES_SPHERE, BYTES_MSPHERE, BYTES_RECT, BYTES_MEDIUM = 32, 20, 40, 24, 8
 
@@ -55,7 +69,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-kind", choices=["auto", "port"], default="auto",
                     help="auto: the reference's own code when oracle/_ref was built, else the oracle")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_bench.json"))
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every host CPU this process may use")
+    ap.add_argument("--pmc-json", default=None,
+                    help="PMC summary to use (default: the newest profiles/*/pmc_summary.json of this build+config)")
     return ap.parse_args()
 
 
@@ -92,6 +108,64 @@ def reference_run(pix, args, threads):
         return None
     r = json.loads(out.stdout.strip().splitlines()[-1])
     return r["seconds"], r["checksum"]
+
+
+def find_pmc(args, world, src_hash):
+    """The PMC summary (tools/profile_bench.sh) that describes this run: the
+    newest one under profiles/ recorded for this config and this build's
+    source hash; failing that the newest for this config, flagged stale."""
+    import glob
+
+    cands = [args.pmc_json] if args.pmc_json else sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.json")))
+    want = [args.width, args.height, args.spp, args.n, world]
+    fresh, stale = None, None
+    for f in cands:
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") != want or "SQ_INSTS_VALU" not in d:
+            continue
+        if d.get("source_hash") == src_hash:
+            fresh = (f, d)
+        else:
+            stale = (f, d)
+    return fresh or stale
+
+
+def roofline(args, world, launch_rays, mean_kms, bpr, src_hash):
+    """VALU-issue roofline of the trace kernel (see the module docstring)."""
+    found = find_pmc(args, world, src_hash)
+    if found is None:
+        return {"bound": "valu", "achieved": None, "peak": VALU_PEAK_G, "unit": "Gwave-instr/s", "frac": None,
+                "traffic": None, "kernel_ms": round(mean_kms, 2), "note": "no PMC summary for this config under profiles/"}
+    path, d = found
+    rays_pmc = d["rays_per_launch"]
+    valu_per_ray = d["SQ_INSTS_VALU"] / rays_pmc
+    achieved = valu_per_ray * launch_rays / (mean_kms * 1e-3) / 1e9
+    lane_util = d["SQ_THREAD_CYCLES_VALU"] / (d["SQ_ACTIVE_INST_VALU"] * 64) if "SQ_THREAD_CYCLES_VALU" in d else None
+    traffic = None
+    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:  # KB; FETCH_SIZE reads half the bytes on gfx950
+        traffic = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024 / rays_pmc * launch_rays
+    frac = achieved / VALU_PEAK_G
+    roof = {"bound": "valu", "achieved": round(achieved, 1), "peak": VALU_PEAK_G, "unit": "Gwave-instr/s",
+            "frac": round(frac, 4),
+            "lane_util": round(lane_util, 4) if lane_util is not None else None,
+            "useful_lane_frac": round(frac * lane_util, 4) if lane_util is not None else None,
+            "traffic": round(traffic) if traffic is not None else None,
+            "valu_per_ray": round(valu_per_ray, 3), "kernel_ms": round(mean_kms, 2),
+            "pmc": os.path.relpath(path, REPO), "pmc_source_hash": d.get("source_hash"),
+            "pmc_matches_build": d.get("source_hash") == src_hash,
+            "peak_def": f"{N_SIMD} SIMD-32 x {CLOCK_GHZ} GHz x 0.5 wave64 VALU instr/cycle"}
+    if "GRBM_GUI_ACTIVE" in d and d.get("kernel_ms_pmc"):
+        roof["clock_ghz_under_pmc"] = round(d["GRBM_GUI_ACTIVE"] / 8 / (d["kernel_ms_pmc"] * 1e-3) / 1e9, 3)
+    if traffic is not None:
+        roof["hbm_gbps"] = round(traffic / (mean_kms * 1e-3) / 1e9, 2)
+        roof["hbm_frac"] = round(traffic / (mean_kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)
+    if bpr is not None:
+        roof["reference_bytes_per_ray"] = round(bpr, 1)
+        roof["reference_equiv_gbps"] = round(bpr * launch_rays / (mean_kms * 1e-3) / 1e9, 1)
+    return roof
 
 
 def cpu_baseline(scene, cam, args, threads):
@@ -199,11 +273,14 @@ def main():
     segs_all, samples_all, elapsed = float(tot[0]), float(tot[1]), float(el[0])
 
     if rank == 0:
-        threads = min(16, os.cpu_count() or 1)
+        threads, cpu_info = rtow.host_threads()
+        if args.cpu_threads:
+            threads = args.cpu_threads
         if args.no_cpu:
             base, bpr, counts = None, None, {}
         elif world == 1:
             base, bpr, counts = cpu_baseline(scene, cam, args, threads)
+            base.update(cpu_info)
         else:  # the CPU baseline is quoted at N=1 only; bytes/ray from a smaller oracle sample
             args.cpu_pixels = max(1, args.cpu_pixels // 10)
             args.cpu_kind = "port"
@@ -211,19 +288,7 @@ def main():
             base = None
         mean_kms = float(np.mean(kms))
         launch_rays = segs / max(args.steps, 1)
-        roof = None
-        if bpr is not None:
-            achieved = bpr * launch_rays / (mean_kms * 1e-3) / 1e9
-            traffic = None
-            if os.path.exists(args.pmc_json):
-                pmc = json.load(open(args.pmc_json))
-                if pmc.get("config") == [W, H, spp, args.n, world]:
-                    traffic = pmc.get("hbm_bytes_per_launch")
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "bytes_per_ray": round(bpr, 1), "kernel_ms": round(mean_kms, 2),
-                    "note": "algorithmic bytes = reference traversal record bytes (SURVEY.md 8d); scene is "
-                            "L2/LDS-resident so real HBM traffic is far lower (traffic field)"}
+        roof = roofline(args, world, launch_rays, mean_kms, bpr, rtow.source_hash())
         out = {
             "metric": "Mray/s + Msample/s, random_scene 1920×1080×1024spp at 1/2/4/8 MI355X",
             "value": round(segs_all / elapsed / 1e6, 2),
@@ -243,6 +308,7 @@ def main():
                        "width": W, "height": H, "spp": spp, "n": args.n, "scene_seed": 1, "render_seed": args.seed,
                        "parallelism": f"tiles8x8 interleaved over {world} rank(s) + RCCL gather to rank 0"},
             "rays_per_sample": round(segs_all / max(samples_all, 1), 4),
+            "rays_per_step": int(segs_all / max(args.steps, 1)),
             "roofline": roof,
             "cpu_baseline": base,
             "oracle_counts": {k: round(v, 3) for k, v in counts.items()},

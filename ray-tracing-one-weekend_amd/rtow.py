@@ -127,6 +127,57 @@ def lib():
     return L
 
 
+def source_hash():
+    """sha256 (first 16 hex digits) of everything librtow_hip.so is compiled
+    from: the device/host sources, the headers and the Makefile (its flags).
+    A PMC summary under profiles/ records the hash of the build it measured,
+    so bench.py can tell whether those counters describe the kernel it runs."""
+    import hashlib
+
+    files = [os.path.join(PKG_DIR, "Makefile")]
+    csrc = os.path.join(PKG_DIR, "csrc")
+    files += [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".cpp", ".h"))]
+    files += [os.path.join(REPO, "include", f) for f in ("rtow.h", "rtow_rng.h")]  # not rtow_reference.hpp
+    h = hashlib.sha256()
+    for f in sorted(files, key=lambda p: os.path.relpath(p, REPO)):
+        h.update(os.path.relpath(f, REPO).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def host_threads():
+    """(threads, info): the host threads this process may use -- the CPUs in
+    its affinity mask, capped by a cgroup v2 CPU quota when one is set (a GPU
+    box shares one machine's CPUs between its GPUs) -- and a dict naming the
+    machine's CPU count, the affinity, the quota and the CPU model."""
+    import math
+
+    machine = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = machine
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    threads = affinity if quota is None else max(1, min(affinity, math.ceil(quota)))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"machine_cpus": machine, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+                     "cpu_model": model}
+
+
 def header_functions():
     """Names of the functions include/rtow.h declares."""
     text = open(HEADER).read()
