@@ -90,171 +90,31 @@ namespace std { using cbrng_engine = ::CbEngine; }
 #undef protected
 
 // ---------------------------------------------------------------------------
-// Scene graph writer: reference objects -> rtow_scene arrays (include/rtow.h
-// documents the canonical order).
-struct GraphWriter {
-    std::vector<rtow_hitable> hit;
-    std::vector<uint32_t> refs;
-    std::vector<rtow_material> mats;
-    std::vector<rtow_texture> texs;
-    std::vector<rtow_image> imgs;
-    std::vector<uint8_t> texels;
-    std::map<const void*, uint32_t> hmap, mmap, tmap, imap;
+// Scene graph: the reference objects flattened by the product's own
+// reference-side adapter (include/rtow_reference.hpp, compiled here in the
+// reference's translation unit exactly as a main.cpp binding would compile
+// it), written as an .scn file (the layout rtow_scene_save writes).
+#include "../include/rtow_reference.hpp"
 
-    static void v3(float* d, const vec3& v) { d[0] = v.x(); d[1] = v.y(); d[2] = v.z(); }
+static void v3(float* d, const vec3& v) { d[0] = v.x(); d[1] = v.y(); d[2] = v.z(); }
 
-    uint32_t image(const unsigned char* data, int nx, int ny) {
-        auto it = imap.find(data);
-        if (it != imap.end()) return it->second;
-        uint32_t idx = (uint32_t)imgs.size();
-        rtow_image im{};
-        im.nx = (uint32_t)nx; im.ny = (uint32_t)ny; im.channels = 3;
-        im.offset = texels.size();
-        texels.insert(texels.end(), data, data + (size_t)nx * ny * 3);
-        imgs.push_back(im);
-        imap[data] = idx;
-        return idx;
-    }
-
-    uint32_t texture(const Texture* t) {
-        auto it = tmap.find(t);
-        if (it != tmap.end()) return it->second;
-        uint32_t idx = (uint32_t)texs.size();
-        texs.push_back(rtow_texture{});
-        tmap[t] = idx;
-        rtow_texture r{};
-        if (auto c = dynamic_cast<const ConstantTexture*>(t)) {
-            r.kind = RTOW_TEX_CONSTANT; v3(r.f, c->_color);
-        } else if (auto k = dynamic_cast<const CheckerTexture*>(t)) {
-            r.kind = RTOW_TEX_CHECKER;
-            r.a = texture(k->_odd);
-            r.b = texture(k->_even);
-        } else if (auto n = dynamic_cast<const NoiseTexture*>(t)) {
-            r.kind = RTOW_TEX_NOISE; r.f[0] = n->_scaled; r.a = n->_filter ? 1 : 0;
-        } else if (auto im = dynamic_cast<const ImageTexture*>(t)) {
-            r.kind = RTOW_TEX_IMAGE; r.a = image(im->_data, im->_nx, im->_ny);
-        } else {
-            std::fprintf(stderr, "unknown texture\n"); std::exit(3);
-        }
-        texs[idx] = r;
-        return idx;
-    }
-
-    uint32_t material(const Material* m) {
-        auto it = mmap.find(m);
-        if (it != mmap.end()) return it->second;
-        uint32_t idx = (uint32_t)mats.size();
-        mats.push_back(rtow_material{});
-        mmap[m] = idx;
-        rtow_material r{};
-        if (auto l = dynamic_cast<const Lambertian*>(m)) {
-            r.kind = RTOW_MAT_LAMBERTIAN; r.texture = texture(l->_albedo);
-        } else if (auto me = dynamic_cast<const Metal*>(m)) {
-            r.kind = RTOW_MAT_METAL; v3(r.albedo, me->_albedo); r.param = me->_fuzz;
-        } else if (auto d = dynamic_cast<const Dielectric*>(m)) {
-            r.kind = RTOW_MAT_DIELECTRIC; r.param = d->_refIndex;
-        } else if (auto dl = dynamic_cast<const DiffuseLight*>(m)) {
-            r.kind = RTOW_MAT_DIFFUSE_LIGHT; r.texture = texture(dl->_emit);
-        } else if (auto is = dynamic_cast<const Isotropic*>(m)) {
-            r.kind = RTOW_MAT_ISOTROPIC; r.texture = texture(is->_albedo);
-        } else {
-            std::fprintf(stderr, "unknown material\n"); std::exit(3);
-        }
-        mats[idx] = r;
-        return idx;
-    }
-
-    uint32_t hitable(const Hitable* h) {
-        auto it = hmap.find(h);
-        if (it != hmap.end()) return it->second;
-        uint32_t idx = (uint32_t)hit.size();
-        hit.push_back(rtow_hitable{});
-        hmap[h] = idx;
-        rtow_hitable r{};
-        if (auto s = dynamic_cast<const Sphere*>(h)) {
-            r.kind = RTOW_HIT_SPHERE; v3(r.f, s->_center); r.f[3] = s->_radius;
-            r.a = material(s->_materialPointer);
-        } else if (auto s = dynamic_cast<const MovingSphere*>(h)) {
-            r.kind = RTOW_HIT_MOVING_SPHERE; v3(r.f, s->_center0); v3(r.f + 3, s->_center1);
-            r.f[6] = s->_time0; r.f[7] = s->_time1; r.f[8] = s->_radius;
-            r.a = material(s->_materialPointer);
-        } else if (auto q = dynamic_cast<const XYRectangle*>(h)) {
-            r.kind = RTOW_HIT_RECT_XY;
-            r.f[0] = q->_x0; r.f[1] = q->_x1; r.f[2] = q->_y0; r.f[3] = q->_y1; r.f[4] = q->_k;
-            r.a = material(q->_material);
-        } else if (auto q = dynamic_cast<const XZRectangle*>(h)) {
-            r.kind = RTOW_HIT_RECT_XZ;
-            r.f[0] = q->_x0; r.f[1] = q->_x1; r.f[2] = q->_z0; r.f[3] = q->_z1; r.f[4] = q->_k;
-            r.a = material(q->_material);
-        } else if (auto q = dynamic_cast<const YZRectangle*>(h)) {
-            r.kind = RTOW_HIT_RECT_YZ;
-            r.f[0] = q->_y0; r.f[1] = q->_y1; r.f[2] = q->_z0; r.f[3] = q->_z1; r.f[4] = q->_k;
-            r.a = material(q->_material);
-        } else if (auto fl = dynamic_cast<const FlipNormals*>(h)) {
-            r.kind = RTOW_HIT_FLIP_NORMALS; r.a = hitable(fl->_hitable);
-        } else if (auto tr = dynamic_cast<const Translate*>(h)) {
-            r.kind = RTOW_HIT_TRANSLATE; v3(r.f, tr->_offset); r.a = hitable(tr->_hitablePointer);
-        } else if (auto ro = dynamic_cast<const RotateY*>(h)) {
-            r.kind = RTOW_HIT_ROTATE_Y; r.f[0] = ro->_sinTheta; r.f[1] = ro->_cosTheta;
-            r.b = ro->_hasBox ? 1 : 0;
-            v3(r.f + 2, ro->_boundBox.min()); v3(r.f + 5, ro->_boundBox.max());
-            r.a = hitable(ro->_pointer);
-        } else if (auto li = dynamic_cast<const HitableList*>(h)) {
-            r.kind = RTOW_HIT_LIST;
-            r.a = (uint32_t)refs.size(); r.b = li->_listSize;
-            refs.resize(refs.size() + li->_listSize);
-            for (uint32_t i = 0; i < li->_listSize; i++) {
-                uint32_t c = hitable(li->_hitableList[i]);
-                refs[r.a + i] = c;
-            }
-        } else if (auto bx = dynamic_cast<const Box*>(h)) {
-            r.kind = RTOW_HIT_BOX; v3(r.f, bx->_pMin); v3(r.f + 3, bx->_pMax);
-            r.a = hitable(bx->_hitableList);
-        } else if (auto bv = dynamic_cast<const BvhNode*>(h)) {
-            r.kind = RTOW_HIT_BVH_NODE; v3(r.f, bv->_box.min()); v3(r.f + 3, bv->_box.max());
-            r.a = hitable(bv->_left);
-            r.b = hitable(bv->_right);
-        } else if (auto cm = dynamic_cast<const ConstantMedium*>(h)) {
-            r.kind = RTOW_HIT_CONSTANT_MEDIUM; r.f[0] = cm->_density;
-            r.a = hitable(cm->_boundary);
-            r.b = material(cm->_phaseFunction);
-        } else {
-            std::fprintf(stderr, "unknown hitable\n"); std::exit(3);
-        }
-        hit[idx] = r;
-        return idx;
-    }
-
-    void write(const char* path, uint32_t root) {
-        FILE* f = std::fopen(path, "wb");
-        if (!f) { std::perror(path); std::exit(2); }
-        rtow_perlin pt{};
-        for (int i = 0; i < 256; i++) {
-            pt.ranfloat[i] = Perlin::randFloat[i];
-            pt.ranvec[i][0] = Perlin::randVector[i].x();
-            pt.ranvec[i][1] = Perlin::randVector[i].y();
-            pt.ranvec[i][2] = Perlin::randVector[i].z();
-            pt.perm_x[i] = Perlin::permX[i];
-            pt.perm_y[i] = Perlin::permY[i];
-            pt.perm_z[i] = Perlin::permZ[i];
-        }
-        uint32_t hdr[10] = {1u, root, (uint32_t)hit.size(), (uint32_t)refs.size(),
-                            (uint32_t)mats.size(), (uint32_t)texs.size(), (uint32_t)imgs.size(), 1u,
-                            0u, 0u};
-        uint64_t ntex = texels.size();
-        std::fwrite("RTOWSCN1", 1, 8, f);
-        std::fwrite(hdr, 4, 10, f);
-        std::fwrite(&ntex, 8, 1, f);
-        std::fwrite(hit.data(), sizeof(rtow_hitable), hit.size(), f);
-        std::fwrite(refs.data(), 4, refs.size(), f);
-        std::fwrite(mats.data(), sizeof(rtow_material), mats.size(), f);
-        std::fwrite(texs.data(), sizeof(rtow_texture), texs.size(), f);
-        std::fwrite(&pt, sizeof(pt), 1, f);
-        std::fwrite(imgs.data(), sizeof(rtow_image), imgs.size(), f);
-        std::fwrite(texels.data(), 1, texels.size(), f);
-        std::fclose(f);
-    }
-};
+static void writeScene(const char* path, const rtow_scene& s) {
+    FILE* f = std::fopen(path, "wb");
+    if (!f) { std::perror(path); std::exit(2); }
+    uint32_t hdr[10] = {1u, s.root, s.n_hitables, s.n_refs, s.n_materials, s.n_textures, s.n_images, 1u, 0u, 0u};
+    uint64_t ntex = s.n_texel_bytes;
+    std::fwrite("RTOWSCN1", 1, 8, f);
+    std::fwrite(hdr, 4, 10, f);
+    std::fwrite(&ntex, 8, 1, f);
+    std::fwrite(s.hitables, sizeof(rtow_hitable), s.n_hitables, f);
+    std::fwrite(s.refs, 4, s.n_refs, f);
+    std::fwrite(s.materials, sizeof(rtow_material), s.n_materials, f);
+    std::fwrite(s.textures, sizeof(rtow_texture), s.n_textures, f);
+    std::fwrite(s.perlin, sizeof(rtow_perlin), 1, f);
+    std::fwrite(s.images, sizeof(rtow_image), s.n_images, f);
+    std::fwrite(s.texels, 1, s.n_texel_bytes, f);
+    std::fclose(f);
+}
 
 // ---------------------------------------------------------------------------
 // Scene composition.  Scenes the reference provides are called directly;
@@ -450,18 +310,36 @@ static Camera* mainCamera(uint32_t W, uint32_t H) {
     return c;
 }
 
-static void writeCamera(const char* path, Camera* c) {
+// the camera's private basis (camera.h:352-379), read directly
+static rtow_camera privateBasis(Camera* c) {
     rtow_camera rc{};
-    GraphWriter::v3(rc.origin, c->_origin);
-    GraphWriter::v3(rc.lower_left_corner, c->_lowerLeftCorner);
-    GraphWriter::v3(rc.horizontal, c->_horizontal);
-    GraphWriter::v3(rc.vertical, c->_vertical);
-    GraphWriter::v3(rc.u, c->_u);
-    GraphWriter::v3(rc.v, c->_v);
-    GraphWriter::v3(rc.w, c->_w);
+    v3(rc.origin, c->_origin);
+    v3(rc.lower_left_corner, c->_lowerLeftCorner);
+    v3(rc.horizontal, c->_horizontal);
+    v3(rc.vertical, c->_vertical);
+    v3(rc.u, c->_u);
+    v3(rc.v, c->_v);
+    v3(rc.w, c->_w);
     rc.lens_radius = c->_lensRadius;
     rc.time0 = c->_time0;
     rc.time1 = c->_time1;
+    return rc;
+}
+
+// the main camera after the frame loop's updates (main.cpp:476/554, 624-628):
+// setOrientationMatrix(rows view/east/down) + setLookFromPoint
+static void orientCamera(Camera* c, const float* v) {
+    mat4x4 m;
+    m.m[0] = vec4(v[3], v[4], v[5], 0.0f);
+    m.m[1] = vec4(v[6], v[7], v[8], 0.0f);
+    m.m[2] = vec4(v[9], v[10], v[11], 0.0f);
+    m.m[3] = vec4(0.0f, 0.0f, 0.0f, 1.0f);
+    c->setOrientationMatrix(m);
+    c->setLookFromPoint(vec3(v[0], v[1], v[2]));
+}
+
+static void writeCamera(const char* path, Camera* c) {
+    const rtow_camera rc = privateBasis(c);
     FILE* f = std::fopen(path, "wb");
     if (!f) { std::perror(path); std::exit(2); }
     std::fwrite(&rc, sizeof(rc), 1, f);
@@ -561,10 +439,10 @@ int main(int argc, char** argv) {
     if (cmd == "dump" && argc >= 4) {
         Opts o = parseOpts(argc, argv, 4);
         Hitable* world = buildWorld(argv[2], o);
-        GraphWriter w;
-        uint32_t root = w.hitable(world);
-        w.write(argv[3], root);
-        std::printf("draws %llu hitables %zu\n", (unsigned long long)CbEngine::total, w.hit.size());
+        rtow_ref::World w(world);
+        if (w.status() != RTOW_OK) { std::fprintf(stderr, "unknown object class\n"); return 3; }
+        writeScene(argv[3], *w.view());
+        std::printf("draws %llu hitables %u\n", (unsigned long long)CbEngine::total, w.view()->n_hitables);
         return 0;
     }
     if (cmd == "camera" && argc >= 5) {
@@ -578,15 +456,26 @@ int main(int argc, char** argv) {
         Camera* c = mainCamera((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]));
         float v[12];
         for (int k = 0; k < 12; k++) v[k] = (float)std::atof(argv[4 + k]);
-        mat4x4 m;
-        m.m[0] = vec4(v[3], v[4], v[5], 0.0f);
-        m.m[1] = vec4(v[6], v[7], v[8], 0.0f);
-        m.m[2] = vec4(v[9], v[10], v[11], 0.0f);
-        m.m[3] = vec4(0.0f, 0.0f, 0.0f, 1.0f);
-        c->setOrientationMatrix(m);
-        c->setLookFromPoint(vec3(v[0], v[1], v[2]));
+        orientCamera(c, v);
         writeCamera(argv[16], c);
         return 0;
+    }
+    if (cmd == "camera_check" && argc >= 16) {
+        // rtow_ref::camera (public getters) against the private basis, for
+        // the main camera and for it after the frame loop's updates
+        Camera* c = mainCamera((uint32_t)std::atoi(argv[2]), (uint32_t)std::atoi(argv[3]));
+        int bad = 0;
+        for (int pass = 0; pass < 2; pass++) {
+            if (pass == 1) {
+                float v[12];
+                for (int k = 0; k < 12; k++) v[k] = (float)std::atof(argv[4 + k]);
+                orientCamera(c, v);
+            }
+            rtow_camera a{}, b = privateBasis(c);
+            if (rtow_ref::camera(*c, &a) != RTOW_OK || std::memcmp(&a, &b, sizeof a) != 0) bad |= 1 << pass;
+        }
+        std::printf("camera_check %s\n", bad ? "DIFFERS" : "identical");
+        return bad ? 1 : 0;
     }
     if (cmd == "render" && argc >= 7) {
         Opts o = parseOpts(argc, argv, 7);
@@ -639,6 +528,47 @@ int main(int argc, char** argv) {
                     sec, pix.size(), (unsigned long long)pix.size() * spp, nt, sum);
         return 0;
     }
+#ifdef RTOW_HARNESS_DROPIN
+    if (cmd == "dropin" && argc >= 7) {
+        // The drop-in as a main.cpp binding would do it: the
+        // reference builds its world and camera (main.cpp:111-137),
+        // rtow_reference.hpp flattens both, librtow_hip.so renders the frame
+        // main.cpp:932-996 would have rendered.  Writes <prefix>.bgra/.lin.
+        Opts o = parseOpts(argc, argv, 7);
+        uint32_t W = (uint32_t)std::atoi(argv[3]), H = (uint32_t)std::atoi(argv[4]);
+        uint32_t spp = (uint32_t)std::atoi(argv[5]);
+        std::string prefix = argv[6];
+        Hitable* world = buildWorld(argv[2], o);
+        Camera* cam = mainCamera(W, H);
+        rtow_ref::World w(world);
+        rtow_camera rc;
+        if (w.status() != RTOW_OK || rtow_ref::camera(*cam, &rc) != RTOW_OK) return 3;
+        rtow_context* ctx = nullptr;
+        int rc2 = rtow_context_create(0, &ctx);
+        if (rc2 == RTOW_OK) rc2 = rtow_scene_upload(ctx, w.view());
+        rtow_params p;
+        rtow_params_default(&p, W, H, spp);
+        p.seed = o.seed;
+        std::vector<uint8_t> bgra((size_t)W * H * 4);
+        std::vector<float> lin((size_t)W * H * 3);
+        rtow_stats st{};
+        if (rc2 == RTOW_OK) rc2 = rtow_render(ctx, &rc, &p, bgra.data(), lin.data(), &st);
+        if (rc2 != RTOW_OK) {
+            std::fprintf(stderr, "dropin: %s (%s)\n", rtow_error_string(rc2), rtow_last_error());
+            return 4;
+        }
+        rtow_context_destroy(ctx);
+        FILE* f = std::fopen((prefix + ".lin").c_str(), "wb");
+        std::fwrite(lin.data(), 4, lin.size(), f);
+        std::fclose(f);
+        f = std::fopen((prefix + ".bgra").c_str(), "wb");
+        std::fwrite(bgra.data(), 1, bgra.size(), f);
+        std::fclose(f);
+        std::printf("{\"segments\": %llu, \"samples\": %llu, \"kernel_ms\": %.3f}\n",
+                    (unsigned long long)st.segments, (unsigned long long)st.samples, st.kernel_ms);
+        return 0;
+    }
+#endif
     std::fprintf(stderr, "bad command\n");
     return 2;
 }

@@ -51,6 +51,10 @@ using namespace rtow_dev;
 // flags (RTOW_TU_SIMPLE, see the Makefile and the end of this section).
 namespace rtow_k {
 
+// Block size of every general-scene kernel: the general traversal (bvh_step,
+// traverse) strides a lane's LDS stack column by BLOCK, so a general kernel
+// must be instantiated with BS == BLOCK (static_assert in trace_kernel); only
+// the simple-scene traversal (trace_simple) takes the block size as BS.
 constexpr int BLOCK = 256;
 constexpr int ROOTCHAIN = 4;  // DevScene::root_chain (simple scenes)
 
@@ -879,7 +883,8 @@ __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uin
             for (uint32_t k = 0; k < T.b; k++) {
                 const uint32_t ref = mkref(DK_RECT, T.a + k);
                 float t;
-                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, bp))) {
+                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, bp)) &&
+                    (!strict || ref_reaches_rect(S, T.a + k, r, tmin))) {
                     bt = t;
                     bp = ref;
                     found = true;
@@ -1297,6 +1302,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     unsigned long long t_mark = PROF ? __builtin_amdgcn_s_memtime() : 0;
     constexpr bool SIMPLE = MODE == 0;
     static_assert(STACK * 64 >= 640, "wave_turbulence scratch lives in the wave's stack columns");
+    static_assert(MODE == 0 || BS == BLOCK, "the general traversal strides its LDS stack by BLOCK");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* s_ranvec = reinterpret_cast<float4*>(smem);
     uint32_t* s_perm = reinterpret_cast<uint32_t*>(smem + 4096);
@@ -3164,6 +3170,10 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.bvh_root = L.bvh_root;
     d.n_node = L.simple ? (uint32_t)L.node.size() : 0u;
     c->has_scene = true;
+    // progressive sums belong to the scene they were rendered from: a new
+    // scene restarts them (rtow_render_progressive)
+    c->accum_spp = 0;
+    c->accum_sig.clear();
     return RTOW_OK;
 }
 

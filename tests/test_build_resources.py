@@ -1,0 +1,60 @@
+"""The shipped gfx950 code (librtow_hip.so's embedded code objects, read by
+tools/codeobj.py -- the binary itself, not a recompilation) keeps the shape the
+kernels were validated in:
+
+* every device function is inlined: the code objects hold kernels only and no
+  kernel contains a call (s_swappc_b64 / s_setpc_b64).  Round 1 saw the
+  general kernels compute wrong results when the tie check was an out-of-line
+  call under a 128-VGPR cap; DESIGN.md ("The out-of-line call hazard") records
+  what the ISA of that build shows;
+* no kernel needs a dynamic stack;
+* scratch (spills) per lane stays within the bound each kernel was measured
+  at: none for the simple-scene kernels, bounded for the general ones.
+CPU only: reads the built library (built by `make`, conftest.py)."""
+import os
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "tools"))
+import codeobj  # noqa: E402
+
+LIB = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "librtow_hip.so")
+
+# scratch bytes per lane allowed for the default (4-wave) general kernels,
+# by MODE (see DESIGN.md "Kernels"); the simple-scene kernels get none
+SCRATCH_BOUND = {0: 0, 2: 16, 4: 64, 3: 192}
+
+
+@pytest.fixture(scope="module")
+def kernels():
+    return codeobj.kernels(LIB)
+
+
+def test_kernels_only_no_calls(kernels):
+    assert kernels
+    for k in kernels:
+        assert k["calls"] == 0, k["name"]
+        assert k["functions"] == [], (k["name"], k["functions"])
+        assert not k["dyn_stack"], k["name"]
+
+
+def test_bench_kernel_has_no_scratch(kernels):
+    hot = [k for k in kernels if codeobj.demangled_params(k["name"]) ==
+           {"MODE": 0, "STACK": 16, "WAVES": 4, "PROF": 0, "BS": 512, "LDSN": 1, "DBG": 0}]
+    assert len(hot) == 1
+    assert hot[0]["scratch"] == 0 and hot[0]["vgpr_spill"] == 0
+    assert hot[0]["vgpr"] <= 128  # 4 waves per SIMD
+
+
+def test_default_kernels_scratch_bounded(kernels):
+    seen = set()
+    for k in kernels:
+        p = codeobj.demangled_params(k["name"])
+        if not p or p["WAVES"] != 4 or p["PROF"] or p["DBG"]:
+            continue
+        seen.add(p["MODE"])
+        assert k["scratch"] <= SCRATCH_BOUND[p["MODE"]], (p, k["scratch"])
+        assert k["vgpr"] <= 128, p
+    assert seen == {0, 2, 3, 4}

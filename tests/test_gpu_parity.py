@@ -61,7 +61,7 @@ def test_segment_count_matches_oracle(gpu_ctx):
     _, _, st = gpu_ctx.render(cam, p)
     _, _, oc = sio.oracle_render(scene.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
                                  sio.RtowParams.from_buffer_copy(bytes(p)))
-    assert abs(st.segments - oc.segments) <= max(2, 1e-3 * oc.segments)
+    assert st.segments == oc.segments
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])

@@ -68,3 +68,22 @@ def test_oriented_camera_render_matches_oracle(scene, gpu_ctx):
                                    sio.RtowParams.from_buffer_copy(bytes(p)))
     rms = np.sqrt(np.mean((lin.reshape(-1, 3).astype(np.float64) - olin) ** 2, axis=0))
     assert (rms <= 1e-4).all(), rms
+
+
+@pytest.mark.gpu
+def test_progressive_restarts_on_scene_upload(gpu_ctx):
+    """Running sums belong to the scene they were rendered from: after a new
+    upload, a progressive frame without reset equals a fresh render of the
+    new scene (not a mix of both scenes)."""
+    W, H = 40, 24
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, 4, seed=1)
+    gpu_ctx.upload(rtow.Scene.build("three_sphere"))
+    gpu_ctx.render_progressive(cam, p, reset=True)
+    gpu_ctx.render_progressive(cam, p)
+    b = rtow.Scene.build("random_ned", n=100, image="synthetic")
+    gpu_ctx.upload(b)
+    _, lin, total, _ = gpu_ctx.render_progressive(cam, p)
+    assert total == 4
+    _, one, _ = gpu_ctx.render(cam, p)
+    assert np.array_equal(lin.view(np.uint32), one.view(np.uint32))

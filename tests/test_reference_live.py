@@ -35,3 +35,21 @@ def test_real_earth_texture_oracle_bit_exact(tmp_path):
     ref = np.fromfile(pre + ".lin", np.float32).reshape(-1, 3)
     assert np.array_equal(lin.view(np.uint32), ref.view(np.uint32))
     assert np.array_equal(bgra.reshape(-1), np.fromfile(pre + ".bgra", np.uint8))
+
+
+def test_restated_random_builder_equals_reference_at_n100(tmp_path):
+    """The config-2 golden scene (n = 487) comes from the harness's restated
+    builder randomSceneNedN (oracle/ref_harness.cpp), because the reference's
+    randomScene_NED() hard-codes n = 100 (scenes.h:122-218).  At n = 100 the
+    restated builder and the reference's own must build the same world: byte
+    for byte the same flattened scene graph, Perlin tables and texels."""
+    env = dict(os.environ, RTOW_SCENE_SEED="1")
+    ref, res = str(tmp_path / "ref.scn"), str(tmp_path / "res.scn")
+    subprocess.run([HARNESS, "dump", "random_ned", ref, "--cwd", REF], env=env, check=True, capture_output=True)
+    subprocess.run([HARNESS, "dump", "random_ned_restated", res, "--n", "100", "--cwd", REF], env=env, check=True,
+                   capture_output=True)
+    a, b = sio.load_scene(ref), sio.load_scene(res)
+    assert a["root"] == b["root"]
+    for k in ("hitables", "refs", "materials", "textures", "images", "perlin", "texels"):
+        assert a[k].tobytes() == b[k].tobytes(), k
+    assert open(ref, "rb").read() == open(res, "rb").read()
