@@ -184,8 +184,11 @@ typedef struct rtow_params {
     uint32_t gi_enable;         /* GLOBAL_ILLUM_EN */
     float sky_gain;             /* SKY_ILLUM_GAIN */
     float gi_gain;              /* GLOBAL_ILLUM_GAIN */
-    uint32_t samples_per_chunk; /* work granularity; 0 = auto (16, or spp/200 if larger, with the last
-                                    spc..2spc samples cut into halving chunks) */
+    uint32_t samples_per_chunk; /* work granularity: a work item is one pixel's chunk of consecutive
+                                    samples, summed in float in sample order (main.cpp:946) and added to
+                                    the pixel's sum in 32.32 fixed point (order-independent, exact);
+                                    0 = auto (16, or spp/200 if larger, with the last spc..2spc samples
+                                    cut into halving chunks) */
     uint64_t seed;              /* render stream seed (rtow_rng.h) */
     uint32_t rank, world;       /* tile partition; world 0 is treated as 1 */
     uint32_t flags;
@@ -197,7 +200,7 @@ typedef struct rtow_stats {
     uint64_t samples;    /* paths (pixel samples) traced */
     uint64_t pixels;     /* pixels this call produced */
     double kernel_ms;    /* trace kernel, HIP events on the render stream */
-    double resolve_ms;   /* chunk-sum + quantise kernel */
+    double resolve_ms;   /* pixel-sum average + quantise kernel */
     double total_ms;     /* whole call, host wall clock */
 } rtow_stats;
 
@@ -314,8 +317,9 @@ int rtow_render(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
  * renders p->spp NEW samples per pixel -- sample indices continue after the
  * ones already accumulated, so the random streams never repeat -- adds them to
  * the context's running sums and writes the average of everything so far.
- * The sums restart when `reset` is set or the camera or any parameter other
- * than spp / samples_per_chunk / blocks_per_cu / flags changed.  total_spp
+ * The sums restart when `reset` is set, a scene is uploaded, or the camera
+ * or any parameter other than spp / samples_per_chunk / blocks_per_cu /
+ * flags changed.  total_spp
  * (may be NULL) receives the samples per pixel accumulated.  F frames of S
  * spp, each one chunk (samples_per_chunk = S, or automatic chunking with
  * S <= 16), give the frame of one rtow_render of F*S spp with

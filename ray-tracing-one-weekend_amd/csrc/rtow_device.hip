@@ -1285,6 +1285,40 @@ __device__ __forceinline__ void shade_segment(const DevScene& S, const DevParams
     }
 }
 
+// ---------------------------------------------------------------------------
+// Pixel sums.  A work item's chunk sum (its samples added in order, in float,
+// as main.cpp:946 adds them) goes into the pixel's sum as an unsigned 32.32
+// fixed-point number: fx = trunc(sum * 2^32), added with 64-bit integer
+// atomics.  Integer addition is associative, so the pixel's sum is the same
+// whatever order the chunks finish in (no [chunk][pixel] buffer, 32 B per
+// pixel, the frame deterministic and independent of the rank split), and
+// progressive frames add into the same sums (any chunking gives the same
+// frame).  The truncation is below 2^-32 per chunk; a chunk sum must stay
+// below 2^24 per channel (every contribution is emitted radiance times a
+// throughput <= 1: the reference's scenes stay below 20 per sample), else
+// the render fails with RTOW_E_UNSUPPORTED (fx_range).  The pixel value is
+// then (float)(fx * 2^-32), averaged as vec3.h:133-139 does.
+constexpr float FX_CHUNK_LIMIT = 16777216.0f;  // 2^24
+__device__ __forceinline__ void fx_add(unsigned long long* dst, F3 acc, uint32_t& range) {
+    const float v[3] = {acc.x, acc.y, acc.z};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float x = v[k];
+        if (!(x >= 0.0f && x < FX_CHUNK_LIMIT)) {  // also NaN
+            range = 1;
+            continue;
+        }
+        // trunc(x * 2^32) exactly: the integer part, then the fraction
+        // (x - floor(x) is exact below 2^24) scaled by 2^32 and truncated
+        const uint32_t hi = (uint32_t)x;
+        const uint32_t lo = (uint32_t)((x - (float)hi) * 4294967296.0f);
+        const unsigned long long q = ((unsigned long long)hi << 32) | lo;
+        if (q) atomicAdd(dst + k, q);
+    }
+}
+
+__device__ __forceinline__ float fx_value(unsigned long long q) { return (float)((double)q * 0x1p-32); }
+
 // MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
 // chain), 2 general scene, 3 general scene with media, 4 general scene with
 // media whose boundaries are spheres or Boxes (no nested general traversal)
@@ -1297,7 +1331,7 @@ constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn) {
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, DevParams P, uint32_t* work,
-                                                       float4* partial, unsigned long long* counters) {
+                                                       unsigned long long* fx, unsigned long long* counters) {
     Prof prof{};
     unsigned long long t_mark = PROF ? __builtin_amdgcn_s_memtime() : 0;
     constexpr bool SIMPLE = MODE == 0;
@@ -1323,7 +1357,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     uint32_t* stk = s_stack + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
 
-    uint32_t item = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0, overflow = 0;
+    uint32_t item = 0, lpx = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0, overflow = 0;
+    uint32_t fx_range = 0;
     uint32_t nseg_dbg = 0;
     bool need_item = true, need_sample = false;
     F3 acc = f3(0, 0, 0), thr = f3(1, 1, 1);
@@ -1350,6 +1385,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 const uint32_t lp = item - chunk * P.n_local_px;
                 uint32_t x, yimg;
                 if (!decode_pixel(P, lp, x, yimg)) continue;  // padding pixel of a partial tile
+                lpx = lp;
                 col = x;
                 row = P.height - 1u - yimg;  // reference row numbering (main.cpp:932)
                 if (chunk < P.n_big) {
@@ -1447,7 +1483,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             acc = add(acc, contrib);
             s++;
             if (s >= s_end) {
-                partial[item] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+                fx_add(fx + 4 * (size_t)lpx, acc, fx_range);
                 need_item = true;
             } else {
                 need_sample = true;
@@ -1459,10 +1495,11 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     uint32_t v = nseg;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    const unsigned long long ov = __ballot(overflow != 0);
+    const unsigned long long ov = __ballot(overflow != 0), orange = __ballot(fx_range != 0);
     if (lane == 0) {
         atomicAdd(&counters[0], (unsigned long long)v);
         if (ov) atomicAdd(&counters[1], 1ull);
+        if (orange) atomicAdd(&counters[13], 1ull);
     }
     if constexpr (PROF) {
         uint32_t vals[9] = {prof.lane_steps, prof.wave_steps, prof.leaf_tests, prof.lane_iters, prof.wave_iters,
@@ -1481,12 +1518,12 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     }
 }
 
-// accum (progressive frames, single rank): running per-pixel sums of all
-// frames; this frame's chunk sums are added to it in order, and the average
-// is over P.sample_base + P.spp samples.
+// fx: the pixel sums (fixed point, see fx_add) of all P.sample_base + P.spp
+// samples -- this frame's chunks added by trace_kernel into the running sums
+// of the earlier progressive frames (sample_base 0: a fresh, zeroed buffer).
 #ifndef RTOW_TU_SIMPLE
-__global__ void resolve_kernel(DevParams P, const float4* partial, uint8_t* slab_bgra, float* slab_lin,
-                               uint8_t* fb_bgra, float* fb_lin, float4* accum) {
+__global__ void resolve_kernel(DevParams P, const unsigned long long* fx, uint8_t* slab_bgra, float* slab_lin,
+                               uint8_t* fb_bgra, float* fb_lin, unsigned long long* counters) {
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= P.n_local_px) return;
     uint32_t x, yimg;
@@ -1500,19 +1537,9 @@ __global__ void resolve_kernel(DevParams P, const float4* partial, uint8_t* slab
         }
         return;
     }
-    float4 a = partial[lp];
-    F3 acc = f3(a.x, a.y, a.z);
-    for (uint32_t c = 1; c < P.n_chunks; c++) {
-        const float4 b = partial[(size_t)c * P.n_local_px + lp];
-        acc = add(acc, f3(b.x, b.y, b.z));
-    }
-    if (accum) {
-        if (P.sample_base) {
-            const float4 prev = accum[lp];
-            acc = add(f3(prev.x, prev.y, prev.z), acc);
-        }
-        accum[lp] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-    }
+    const unsigned long long* sum = fx + 4 * (size_t)lp;
+    if ((sum[0] | sum[1] | sum[2]) >> 63) atomicAdd(&counters[13], 1ull);  // beyond 2^31 per channel
+    const F3 acc = f3(fx_value(sum[0]), fx_value(sum[1]), fx_value(sum[2]));
     const float k = (float)(1.0 / (double)(float)(P.sample_base + P.spp));  // vec3.h:133-139
     const F3 lin = f3(acc.x * k, acc.y * k, acc.z * k);
     const float sq[3] = {sqrtf(lin.x), sqrtf(lin.y), sqrtf(lin.z)};
@@ -1554,7 +1581,7 @@ __global__ void assemble_kernel(uint32_t W, uint32_t H, uint32_t world, uint32_t
 // The simple-scene kernel the bench runs (random scene, BVH in LDS) is
 // compiled in its own translation unit with -amdgpu-sched-strategy=
 // iterative-ilp (+2.8 % there, but -3..-6 % on the general kernels).
-#define RTOW_SIMPLE_HOT_ARGS DevScene, DevCam, DevParams, uint32_t*, float4*, unsigned long long*
+#define RTOW_SIMPLE_HOT_ARGS DevScene, DevCam, DevParams, uint32_t*, unsigned long long*, unsigned long long*
 #ifdef RTOW_TU_SIMPLE
 template __global__ void trace_kernel<0, 16, 4, false, 512, true, false>(RTOW_SIMPLE_HOT_ARGS);
 #else
@@ -2788,15 +2815,16 @@ struct rtow_context {
     bool has_scene = false;
     // work buffers
     void* d_work = nullptr;  // [0] work counter (u32) | [8..] u64 counters
-    float4* d_partial = nullptr;
-    size_t partial_bytes = 0;
+    unsigned long long* d_fx = nullptr;  // pixel sums of one render (fx_add), 32 B per local pixel
+    size_t fx_bytes = 0;
     uint8_t* d_fb = nullptr;  // rtow_render: BGRA frame + linear frame
     size_t fb_bytes = 0;
     // rtow_render_progressive: running sums, samples so far, what they were rendered with
-    float4* d_accum = nullptr;
+    unsigned long long* d_accum = nullptr;  // progressive frames' running pixel sums (same layout)
     size_t accum_bytes = 0;
     uint32_t accum_spp = 0;
     std::vector<uint8_t> accum_sig;
+    unsigned long long* fx_cur = nullptr;  // the sums the launch in flight adds into (d_fx or d_accum)
 };
 
 namespace {
@@ -2845,7 +2873,7 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
     hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>), dim3(grid), dim3(BS), lds, st, c->scene,
                        cam, P,
-                       (uint32_t*)c->d_work, c->d_partial, (unsigned long long*)((uint8_t*)c->d_work + 8));
+                       (uint32_t*)c->d_work, c->fx_cur, (unsigned long long*)((uint8_t*)c->d_work + 8));
     HIP_TRY(hipGetLastError());
     return RTOW_OK;
 }
@@ -2954,7 +2982,7 @@ DevCam makeCam(const rtow_camera* cam) {
 
 // trace + resolve on `st`; outputs may be NULL
 int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, uint8_t* slab_bgra, float* slab_lin,
-               uint8_t* fb_bgra, float* fb_lin, hipStream_t st, rtow_stats* stats, float4* accum = nullptr,
+               uint8_t* fb_bgra, float* fb_lin, hipStream_t st, rtow_stats* stats, unsigned long long* accum = nullptr,
                uint32_t sample_base = 0) {
     auto t0 = std::chrono::steady_clock::now();
     if (!c || !cam) return set_error(RTOW_E_INVALID, "NULL context or camera");
@@ -2964,9 +2992,15 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
     if (rc) return rc;
     P.sample_base = sample_base;
     HIP_TRY(hipSetDevice(c->device));
-    size_t need = (size_t)P.n_chunks * P.n_local_px * sizeof(float4);
-    rc = ensure((void**)&c->d_partial, &c->partial_bytes, std::max<size_t>(need, 16));
-    if (rc) return rc;
+    const size_t fx_need = (size_t)P.n_local_px * 4 * sizeof(unsigned long long);
+    if (accum) {  // progressive: the running sums (zeroed by the caller when they restart)
+        c->fx_cur = accum;
+    } else {
+        rc = ensure((void**)&c->d_fx, &c->fx_bytes, std::max<size_t>(fx_need, 32));
+        if (rc) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_fx, 0, fx_need, st));
+        c->fx_cur = c->d_fx;
+    }
     HIP_TRY(hipMemsetAsync(c->d_work, 0, 128, st));
     const DevCam dc = makeCam(cam);
     HIP_TRY(hipEventRecord(c->ev[0], st));
@@ -2976,12 +3010,12 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
     }
     HIP_TRY(hipEventRecord(c->ev[1], st));
     if (P.n_local_px) {
-        hipLaunchKernelGGL(resolve_kernel, dim3((P.n_local_px + 255) / 256), dim3(256), 0, st, P, c->d_partial, slab_bgra,
-                           slab_lin, fb_bgra, fb_lin, accum);
+        hipLaunchKernelGGL(resolve_kernel, dim3((P.n_local_px + 255) / 256), dim3(256), 0, st, P, c->fx_cur, slab_bgra,
+                           slab_lin, fb_bgra, fb_lin, (unsigned long long*)((uint8_t*)c->d_work + 8));
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[2], st));
-    unsigned long long host_ctr[13] = {};
+    unsigned long long host_ctr[14] = {};
     HIP_TRY(hipMemcpyAsync(host_ctr, (uint8_t*)c->d_work + 8, sizeof host_ctr, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (c->profile && host_ctr[3])
@@ -3003,6 +3037,9 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
                      (double)host_ctr[7], (double)host_ctr[8],
                      (double)host_ctr[7] / (double)(host_ctr[7] + host_ctr[8]));
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
+    if (host_ctr[13])
+        return set_error(RTOW_E_UNSUPPORTED, "pixel sum out of the fixed-point range (a chunk of samples summed to "
+                                             ">= 2^24 or NaN, or a pixel to >= 2^31)");
     if (stats) {
         float k = 0, r = 0;
         HIP_TRY(hipEventElapsedTime(&k, c->ev[0], c->ev[1]));
@@ -3079,7 +3116,7 @@ int rtow_context_destroy(rtow_context* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_work) (void)hipFree(c->d_work);
-    if (c->d_partial) (void)hipFree(c->d_partial);
+    if (c->d_fx) (void)hipFree(c->d_fx);
     if (c->d_fb) (void)hipFree(c->d_fb);
     if (c->d_accum) (void)hipFree(c->d_accum);
     for (auto& ev : c->ev)
@@ -3222,10 +3259,11 @@ int rtow_render_progressive(rtow_context* c, const rtow_camera* cam, const rtow_
     size_t need = npx * 4 + npx * 12 + 256;
     int rc = ensure((void**)&c->d_fb, &c->fb_bytes, need);
     if (rc) return rc;
-    const size_t acc_need = (size_t)rtow_rank_tile_count(q.width, q.height, 0, 1) * 64 * sizeof(float4);
+    const size_t acc_need = (size_t)rtow_rank_tile_count(q.width, q.height, 0, 1) * 64 * 4 * sizeof(unsigned long long);
     if (c->accum_bytes < acc_need) c->accum_spp = 0;
     rc = ensure((void**)&c->d_accum, &c->accum_bytes, acc_need);
     if (rc) return rc;
+    if (c->accum_spp == 0) HIP_TRY(hipMemsetAsync(c->d_accum, 0, acc_need, c->stream));
     uint8_t* d_bgra = c->d_fb;
     float* d_lin = (float*)(c->d_fb + ((npx * 4 + 255) & ~size_t(255)));
     rc = renderCore(c, cam, &q, nullptr, nullptr, d_bgra, linear_out ? d_lin : nullptr, c->stream, stats, c->d_accum,
