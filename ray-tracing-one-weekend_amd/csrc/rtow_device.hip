@@ -431,6 +431,8 @@ struct Prof {
     uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
     uint32_t disc_pos, accepted, wave_mixed, wave_sph;  // sphere slots with disc > 0 / taken; waves running both slot paths / any sphere path
     unsigned long long cyc_trav, cyc_other;  // wave cycles (s_memtime) in traversal / everything else
+    // general scenes: wave cycles per top-level item (first 8), in finalize, and the item visits
+    unsigned long long cyc_item[8], cyc_fin, visits_item[8], cyc_chain;
 };
 // General scenes: does leaf `cand`, hit at exactly the t of the current best
 // leaf `best`, take the record in the reference?  (assignTieKeys)
@@ -500,6 +502,56 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
     }
     if (li) return lr.x;
     if (ri) return lr.y;
+    return mkref(DK_NONE, 0);
+}
+
+// The DK_BVH step of a general scene in SAH mode (DevScene::gnode): the
+// node's DNode twin, sphere children inline (tested right here, no box test
+// and no second fetch), any other child a box slot.  Same contract as
+// bvh_step: the nearer hit inner child is returned, the farther pushed;
+// exact ties between leaves by the tie keys.
+template <int STACK>
+__device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
+                                               float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
+                                               uint32_t& overflow) {
+    const float4* np = reinterpret_cast<const float4*>(S.node + idx);
+    const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
+    const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
+    const float btc = cull_bound(bt);
+    float ta = 0.0f, tb = 0.0f;
+    bool ha = false, hb = false;
+    if ((refb >> KIND_SHIFT) == DK_SPHERE) {  // slot b (the right child) first
+        const F3 c = add(f3(b0.x, b0.y, b0.z), scl(r.time, f3(b1.x, b1.y, b1.z)));
+        float t;
+        if (sph_root(c, b0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refb, best)))) {
+            bt = t;
+            best = refb;
+        }
+    } else {
+        hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) != DK_NONE;
+    }
+    if ((refa >> KIND_SHIFT) == DK_SPHERE) {
+        const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
+        float t;
+        if (sph_root(c, a0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refa, best)))) {
+            bt = t;
+            best = refa;
+        }
+    } else {
+        ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) != DK_NONE;
+    }
+    if (ha && hb) {
+        const bool afirst = ta <= tb;
+        if (sp < STACK) {
+            stk[sp * BLOCK] = afirst ? refb : refa;
+            sp++;
+        } else {
+            overflow = 1;
+        }
+        return afirst ? refa : refb;
+    }
+    if (ha) return refa;
+    if (hb) return refb;
     return mkref(DK_NONE, 0);
 }
 
@@ -655,9 +707,9 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
 // ANYB: media whose boundary needs the general traversal may occur (MB_ANY);
 // without them the kernel carries no nested traversal (fewer registers).
 template <bool MEDIA, int STACK, bool ANYB = true>
-__device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
-                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev,
-                         bool strict = false);
+__device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin,
+                                         float tmax, uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow,
+                                         uint32_t prev, bool strict = false, Prof* prof = nullptr);
 
 template <int STACK, bool ANYB>
 __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, const Ray& wray,
@@ -731,9 +783,9 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
 // `prev`: the leaf that holds tmax from before the call (DK_NONE: none), for
 // exact ties at tmax.
 template <bool MEDIA, int STACK, bool ANYB>
-__device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin, float tmax,
-                         uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow, uint32_t prev,
-                         bool strict) {
+__device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin,
+                                         float tmax, uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow,
+                                         uint32_t prev, bool strict, Prof* prof) {
     Ray r = chain_ray(S, chain0, wray);
     SlabRay q = slab_ray(r);
     float a = dot(r.d, r.d);
@@ -745,11 +797,17 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
     int sp = sp0;
     while (true) {
         uint32_t kind = cur >> KIND_SHIFT;
+        if (prof) {  // instrumented kernel only (a null pointer otherwise: folded away)
+            prof->lane_steps++;
+            if (first_active_lane()) prof->wave_steps++;
+            if (kind == DK_BVH) prof->leaf_tests++;
+        }
         const uint32_t idx = cur & INDEX_MASK;
         if (kind == DK_BVH) {
             const uint32_t before = best.prim;
             uint32_t b = before;
-            const uint32_t nxt = S.unit_time
+            const uint32_t nxt = S.gnode ? dnode_step<STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
+                                 : S.unit_time
                                      ? bvh_step<true, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
                                      : bvh_step<false, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow);
             if (b != before) {
@@ -760,14 +818,15 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
                 cur = nxt;
                 continue;
             }
-        } else if (kind == DK_SPHERE) {
+        } else if (kind == DK_SPHERE || kind == DK_MSPHERE) {
             float t;
             const Sph s = load_sph(S.sph + idx);
             const F3 c = S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time);
+            const uint32_t ref = mkref(DK_SPHERE, idx);
             if (sph_root(c, s.r, r, a, ra, tmin, t) &&
-                (t < bt || (t == bt && wins_tie(S, cur, best.prim)))) {
+                (t < bt || (t == bt && wins_tie(S, ref, best.prim)))) {
                 bt = t;
-                best.prim = cur;
+                best.prim = ref;
                 found = true;
             }
         } else if (kind == DK_RECT) {
@@ -846,9 +905,11 @@ __device__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint
 // The closest hit of a general scene whose root (below its instances) is a
 // list, scanned as hitableList.h:20-38 does: items in order, tmax the closest
 // hit so far.  The loop is uniform across the wave (see DTop).
-template <bool MEDIA, int STACK, bool ANYB>
+// MEDIA / ANYB: media below the top level (the general traversal asks them);
+// TOPMED: media as top-level items (TOP_MEDIUM).
+template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false>
 __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
-                             uint32_t& overflow, bool strict) {
+                             uint32_t& overflow, bool strict, Prof* prof = nullptr) {
     float bt = FLT_MAX;
     uint32_t bp = mkref(DK_NONE, 0);
     bool found = false;
@@ -857,27 +918,46 @@ __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uin
     uint32_t dx = 0, dy = 0, dz = 0;
     F3 inv = f3(0, 0, 0);
     float a = 0, ra = 0;
+    uint32_t last_chain = ~0u;  // the chain `r` was computed for
+    Ray r = wray;
     const uint32_t n = S.n_top ? S.n_top : 1u;  // no top-level list: the whole graph is one item
+    unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     for (uint32_t j = 0; j < n; j++) {
+        if constexpr (PROF) {  // the previous item's wave cycles
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            if (j > 0 && j <= 8) prof->cyc_item[j - 1] += t1 - t0;
+            if (j < 8 && first_active_lane()) prof->visits_item[j]++;
+            t0 = t1;
+        }
         const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
         if (T.kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
             Best b;
-            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp, strict)) {
+            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp, strict,
+                                             PROF ? prof : nullptr)) {
                 bt = b.t;
                 bp = b.prim;
                 found = true;
             }
             continue;
         }
-        const Ray r = chain_ray(S, T.chain, wray);
-        if (!have || __float_as_uint(r.d.x) != dx || __float_as_uint(r.d.y) != dy || __float_as_uint(r.d.z) != dz) {
-            have = true;
-            dx = __float_as_uint(r.d.x);
-            dy = __float_as_uint(r.d.y);
-            dz = __float_as_uint(r.d.z);
-            inv = inv_dir(r.d);
-            a = dot(r.d, r.d);
-            ra = 1.0f / a;
+        unsigned long long tc = PROF ? __builtin_amdgcn_s_memtime() : 0;
+        // consecutive items in one frame (a room's walls) share the ray
+        if (T.chain != last_chain) {
+            last_chain = T.chain;
+            r = chain_ray(S, T.chain, wray);
+            if (!have || __float_as_uint(r.d.x) != dx || __float_as_uint(r.d.y) != dy || __float_as_uint(r.d.z) != dz) {
+                have = true;
+                dx = __float_as_uint(r.d.x);
+                dy = __float_as_uint(r.d.y);
+                dz = __float_as_uint(r.d.z);
+                inv = inv_dir(r.d);
+                a = dot(r.d, r.d);
+                ra = 1.0f / a;
+            }
+        }
+        if constexpr (PROF) {
+            __builtin_amdgcn_s_waitcnt(0);
+            prof->cyc_chain += __builtin_amdgcn_s_memtime() - tc;
         }
         if (T.kind == TOP_RECTS) {
             for (uint32_t k = 0; k < T.b; k++) {
@@ -890,6 +970,13 @@ __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uin
                     found = true;
                 }
             }
+        } else if (TOPMED && T.kind == TOP_MEDIUM) {
+            // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
+            // so far as tmax, in the medium's frame; it draws as the reference
+            if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) {
+                bp = mkref(DK_MEDIUM, T.a);
+                found = true;
+            }
         } else if (T.kind == TOP_SPHERE) {
             const uint32_t ref = mkref(DK_SPHERE, T.a);
             const Sph sp = load_sph(S.sph + T.a);
@@ -901,6 +988,9 @@ __device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uin
                 found = true;
             }
         }
+    }
+    if constexpr (PROF) {
+        if (n <= 8) prof->cyc_item[n - 1] += __builtin_amdgcn_s_memtime() - t0;
     }
     best.t = bt;
     best.prim = bp;
@@ -1321,12 +1411,18 @@ __device__ __forceinline__ float fx_value(unsigned long long q) { return (float)
 
 // MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
 // chain), 2 general scene, 3 general scene with media, 4 general scene with
-// media whose boundaries are spheres or Boxes (no nested general traversal)
+// media whose boundaries are spheres or Boxes (no nested general traversal),
+// 5 general scene whose media are all top-level items with such boundaries
+// (asked by the top-level scan only: the general traversal carries no media)
 // All LDS is one dynamic region (16-B aligned carve, no static __shared__):
 // Perlin ranvec (4 KB) | perms (1 KB) | traversal stack STACK x BS words |
-// (LDSN) the DNode array of a simple scene.
-constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn) {
-    return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0);
+// (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
+// words: the path state the traversal does not read, parked while it runs
+// (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
+constexpr int COLD = 12;
+constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
+    return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
+           (general ? (size_t)COLD * BS * 4 : 0);
 }
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
@@ -1355,6 +1451,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     __syncthreads();
     const Tables T{s_ranvec, s_perm};
     uint32_t* stk = s_stack + threadIdx.x;
+    uint32_t* cold = reinterpret_cast<uint32_t*>(smem + 5120 + (size_t)STACK * BS * 4) + threadIdx.x;  // general only
     const uint32_t lane = threadIdx.x & 63u;
 
     uint32_t item = 0, lpx = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0, overflow = 0;
@@ -1435,6 +1532,19 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             }
             if (hit) finalize<true>(S, prim, bt, ray, rec);
         } else {
+            // park the path state the traversal does not need (COLD)
+            cold[0 * BS] = __float_as_uint(acc.x);
+            cold[1 * BS] = __float_as_uint(acc.y);
+            cold[2 * BS] = __float_as_uint(acc.z);
+            cold[3 * BS] = __float_as_uint(thr.x);
+            cold[4 * BS] = __float_as_uint(thr.y);
+            cold[5 * BS] = __float_as_uint(thr.z);
+            cold[6 * BS] = lpx;
+            cold[7 * BS] = s;
+            cold[8 * BS] = s_end;
+            cold[9 * BS] = col;
+            cold[10 * BS] = row;
+            cold[11 * BS] = depth;
             Best best;
             best.prim = 0;
             // a winning rectangle the reference would not have reached (its
@@ -1443,7 +1553,19 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             const Rng rng0 = rng;
             bool strict = false;
             while (true) {
-                hit = traverse_top<MODE >= 3, STACK, MODE == 3>(S, ray, 0.001f, stk, rng, best, overflow, strict);
+                if constexpr (PROF) {
+                    const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                    prof.cyc_other += t_now - t_mark;
+                    t_mark = t_now;
+                }
+                hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF>(S, ray, 0.001f, stk, rng,
+                                                                                           best, overflow, strict,
+                                                                                           &prof);
+                if constexpr (PROF) {
+                    const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                    prof.cyc_trav += t_now - t_mark;
+                    t_mark = t_now;
+                }
                 if (!strict && hit && (best.prim >> KIND_SHIFT) == DK_RECT &&
                     ref_skips_hit(S, best.prim & INDEX_MASK, ray, best.t, 0.001f)) {
                     rng = rng0;
@@ -1453,6 +1575,19 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 break;
             }
             if (hit) finalize<false>(S, best.prim, best.t, ray, rec);
+            acc = f3(__uint_as_float(cold[0 * BS]), __uint_as_float(cold[1 * BS]), __uint_as_float(cold[2 * BS]));
+            thr = f3(__uint_as_float(cold[3 * BS]), __uint_as_float(cold[4 * BS]), __uint_as_float(cold[5 * BS]));
+            lpx = cold[6 * BS];
+            s = cold[7 * BS];
+            s_end = cold[8 * BS];
+            col = cold[9 * BS];
+            row = cold[10 * BS];
+            depth = cold[11 * BS];
+            if constexpr (PROF) {
+                const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                prof.cyc_fin += t_now - t_mark;
+                t_mark = t_now;
+            }
         }
         if constexpr (DBG) {
             if (col == P.dbg_col && row == P.dbg_row && s == P.dbg_sample) {
@@ -1514,6 +1649,14 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         if (lane == 0) {  // s_memtime is per wave: lane 0's copy is the wave's
             atomicAdd(&counters[7], prof.cyc_trav);
             atomicAdd(&counters[8], prof.cyc_other);
+            if constexpr (!SIMPLE) {
+                for (int k = 0; k < 8; k++) {
+                    atomicAdd(&counters[16 + k], prof.cyc_item[k]);
+                    atomicAdd(&counters[24 + k], prof.visits_item[k]);
+                }
+                atomicAdd(&counters[32], prof.cyc_fin);
+                atomicAdd(&counters[33], prof.cyc_chain);
+            }
         }
     }
 }
@@ -1626,6 +1769,8 @@ struct HostLayout {
     uint32_t chain_need = 0;
     bool has_media = false;
     bool media_any = false;
+    bool gnode = false;
+    bool media_nested = false;  // a medium the general traversal must ask (not a TOP_MEDIUM item)
     bool simple = false;
     bool unit_time = true;
     uint32_t root_chain_n = 0;
@@ -2613,9 +2758,57 @@ void buildTop(HostLayout& L) {
             if (one) t = DTop{TOP_RECTS, r.first, r.count, L.rect[r.first].chain};
         } else if (k == DK_SPHERE) {
             t = DTop{TOP_SPHERE, i, 0, L.sph[i].chain};
+        } else if (k == DK_MEDIUM && L.med[i].bkind != MB_ANY) {
+            t = DTop{TOP_MEDIUM, i, 0, L.med[i].chain};
         }
         L.top.push_back(t);
     }
+}
+
+// The DNode twin of every DBvh of a general scene (DevScene::gnode): sphere
+// children with time0 = 0, time1 = 1 inline (center(time) = c0 + time * dc
+// exactly, as sph_center computes it for them), other children as box slots
+// (a non-inlined sphere as DK_MSPHERE); a lone sphere child goes to slot b,
+// as in sahBuild.
+void buildGeneralNodes(HostLayout& L) {
+    L.node.assign(L.bvh.size(), DNode{});
+    for (size_t i = 0; i < L.bvh.size(); i++) {
+        const DBvh& b = L.bvh[i];
+        uint32_t refs[2] = {b.left, b.right};
+        float box[2][6];
+        for (int k = 0; k < 2; k++) {
+            box[k][0] = b.xs[2 * k], box[k][1] = b.ys[2 * k], box[k][2] = b.zs[2 * k];
+            box[k][3] = b.xs[2 * k + 1], box[k][4] = b.ys[2 * k + 1], box[k][5] = b.zs[2 * k + 1];
+        }
+        bool inl[2];
+        for (int k = 0; k < 2; k++) {
+            inl[k] = false;
+            if ((refs[k] >> KIND_SHIFT) == DK_SPHERE) {
+                const DSphere& sp = L.sph[refs[k] & INDEX_MASK];
+                inl[k] = sp.t0 == 0.0f && sp.t1 == 1.0f;
+                if (!inl[k]) refs[k] = mkref(DK_MSPHERE, refs[k] & INDEX_MASK);
+            }
+        }
+        if (inl[0] && !inl[1]) {
+            std::swap(refs[0], refs[1]);
+            std::swap(inl[0], inl[1]);
+            for (int q = 0; q < 6; q++) std::swap(box[0][q], box[1][q]);
+        }
+        DNode& d = L.node[i];
+        for (int k = 0; k < 2; k++) {
+            float* f = k == 0 ? d.a : d.b;
+            (k == 0 ? d.ref_a : d.ref_b) = refs[k];
+            if (inl[k]) {
+                const DSphere& sp = L.sph[refs[k] & INDEX_MASK];
+                f[0] = sp.c0[0], f[1] = sp.c0[1], f[2] = sp.c0[2], f[3] = sp.r;
+                f[4] = sp.dc[0], f[5] = sp.dc[1], f[6] = sp.dc[2];
+            } else {
+                for (int q = 0; q < 6; q++) f[q] = box[k][q];
+                f[6] = 0.0f;
+            }
+        }
+    }
+    L.gnode = !L.bvh.empty();
 }
 
 bool textureNeedsUv(const rtow_scene& s, uint32_t ti, int guard = 0) {
@@ -2752,7 +2945,6 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         Bounds bd2{L};
         L.stack_need = bd2.need(L.root, false).first;
     }
-    if (!L.simple && tree == RTOW_TREE_SAH) buildTop(L);
     // how each medium's boundary is queried (DMedium::bkind); REFERENCE mode
     // keeps the general traversal for all of them
     for (DMedium& M : L.med) {
@@ -2779,6 +2971,19 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
             }
         }
         if (M.bkind == MB_ANY) L.media_any = true;
+    }
+    if (!L.simple && tree == RTOW_TREE_SAH) {
+        buildTop(L);
+        buildGeneralNodes(L);
+    }
+    // media the top-level scan does not ask (TOP_MEDIUM) are asked inside the
+    // general traversal
+    {
+        std::vector<bool> top_med(L.med.size(), false);
+        for (const DTop& t : L.top)
+            if (t.kind == TOP_MEDIUM) top_med[t.a] = true;
+        for (size_t i = 0; i < L.med.size(); i++)
+            if (!top_med[i]) L.media_nested = true;
     }
     if (L.sph_key.empty()) L.sph_key.push_back(0);
     if (L.rect_key.empty()) L.rect_key.push_back(0);
@@ -2849,7 +3054,7 @@ int ensure(void** p, size_t* have, size_t need) {
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
-    const size_t lds = lds_bytes(STACK, BS, c->scene.n_node, LDSN);
+    const size_t lds = lds_bytes(STACK, BS, c->scene.n_node, LDSN, MODE != 0);
     // the occupancy query is host work between the launch events: once per
     // (kernel, LDS size) per process
     static std::mutex mu;
@@ -2883,6 +3088,9 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
 template <int MODE, int STACK>
 int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     if (c->dbg_out) return launchTrace<MODE, STACK, 1, false, BLOCK, false, true>(c, cam, P, bpc, st);
+    if constexpr (MODE != 0 && STACK <= 32) {
+        if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
+    }
     if constexpr (STACK <= 32) {
         if constexpr (MODE == 0 && STACK == 16) {
             if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
@@ -2892,7 +3100,7 @@ int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
         }
         if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
         if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
-        if constexpr (MODE != 4) {
+        if constexpr (MODE == 0 || MODE == 2 || MODE == 3) {
             if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
             if (c->waves == 2) return launchTrace<MODE, STACK, 2>(c, cam, P, bpc, st);
         }
@@ -2904,6 +3112,10 @@ template <int MODE>
 int launchStack(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const uint32_t need = c->scene.stack_need;
     if (need <= 16) return launchWaves<MODE, 16>(c, cam, P, bpc, st);
+    // general kernels: 20 entries keep 4 blocks of 256 per CU within LDS
+    // (tables + stack + COLD: 37 KB a block); final_ned needs 17
+    if constexpr (MODE != 0)
+        if (need <= 20) return launchWaves<MODE, 20>(c, cam, P, bpc, st);
     if (need <= 32) return launchWaves<MODE, 32>(c, cam, P, bpc, st);
     if (need <= 64) return launchWaves<MODE, 64>(c, cam, P, bpc, st);
     return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
@@ -2913,6 +3125,7 @@ int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32
     const DevScene& d = c->scene;
     if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
     if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
+    if (!d.media_any && !d.media_nested) return launchStack<5>(c, cam, P, bpc, st);
     if (!d.media_any) return launchStack<4>(c, cam, P, bpc, st);
     return launchStack<3>(c, cam, P, bpc, st);
 }
@@ -3001,7 +3214,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
         HIP_TRY(hipMemsetAsync(c->d_fx, 0, fx_need, st));
         c->fx_cur = c->d_fx;
     }
-    HIP_TRY(hipMemsetAsync(c->d_work, 0, 128, st));
+    HIP_TRY(hipMemsetAsync(c->d_work, 0, 512, st));
     const DevCam dc = makeCam(cam);
     HIP_TRY(hipEventRecord(c->ev[0], st));
     if (P.n_items) {
@@ -3015,7 +3228,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[2], st));
-    unsigned long long host_ctr[14] = {};
+    unsigned long long host_ctr[40] = {};
     HIP_TRY(hipMemcpyAsync(host_ctr, (uint8_t*)c->d_work + 8, sizeof host_ctr, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (c->profile && host_ctr[3])
@@ -3035,7 +3248,19 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
     if (c->profile && host_ctr[7])
         std::fprintf(stderr, "rtow-profile: wave cycles traversal %.3g other %.3g (traversal share %.3f)\n",
                      (double)host_ctr[7], (double)host_ctr[8],
-                     (double)host_ctr[7] / (double)(host_ctr[7] + host_ctr[8]));
+                     (double)host_ctr[7] / (double)(host_ctr[7] + host_ctr[8] + host_ctr[32]));
+    if (c->profile && host_ctr[32]) {
+        const double tot = (double)(host_ctr[7] + host_ctr[8] + host_ctr[32]);
+        std::fprintf(stderr, "rtow-profile: general traversal iterations lane %llu wave %llu (SIMD eff %.3f, %.2f per "
+                             "ray, node steps %.2f per ray)\n",
+                     host_ctr[2], host_ctr[3], (double)host_ctr[2] / (64.0 * std::max(1ull, host_ctr[3])),
+                     (double)host_ctr[2] / std::max(1ull, host_ctr[0]), (double)host_ctr[4] / std::max(1ull, host_ctr[0]));
+        std::fprintf(stderr, "rtow-profile: general: finalize %.3f of wave cycles; per top item (share, wave visits):",
+                     host_ctr[32] / tot);
+        for (int k = 0; k < 8; k++)
+            if (host_ctr[24 + k]) std::fprintf(stderr, " [%d] %.3f %llu", k, host_ctr[16 + k] / tot, host_ctr[24 + k]);
+        std::fprintf(stderr, " | chain_ray+constants of in-place items %.3f\n", host_ctr[33] / tot);
+    }
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
     if (host_ctr[13])
         return set_error(RTOW_E_UNSUPPORTED, "pixel sum out of the fixed-point range (a chunk of samples summed to "
@@ -3105,7 +3330,7 @@ int rtow_context_create(int device, rtow_context** out) {
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
-    if ((e = hipMalloc(&c->d_work, 128)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    if ((e = hipMalloc(&c->d_work, 512)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     *out = c;
     return RTOW_OK;
 }
@@ -3132,6 +3357,13 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
     int rc = buildLayout(*s, L);
     if (rc) return rc;
     if (L.stack_need > 64) return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
+    if (std::getenv("RTOW_LAYOUT_INFO"))
+        std::fprintf(stderr,
+                     "rtow-layout: simple %d gnode %d nodes %zu bvh %zu spheres %zu rects %zu lists %zu insts %zu media %zu "
+                     "top %zu stack_need %u chain_need %u media_nested %d media_any %d\n",
+                     (int)L.simple, (int)L.gnode, L.node.size(), L.bvh.size(), L.sph.size(), L.rect.size(), L.list.size(),
+                     L.inst.size(), L.med.size(), L.top.size(), L.stack_need, L.chain_need, (int)L.media_nested,
+                     (int)L.media_any);
     if (stack_need) *stack_need = L.stack_need;
     if (chain_need) *chain_need = L.chain_need;
     return RTOW_OK;
@@ -3206,6 +3438,8 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     for (int k = 0; k < 4; k++) d.root_chain[k] = L.root_chain[k];
     d.bvh_root = L.bvh_root;
     d.n_node = L.simple ? (uint32_t)L.node.size() : 0u;
+    d.gnode = L.gnode ? 1u : 0u;
+    d.media_nested = L.media_nested ? 1u : 0u;
     c->has_scene = true;
     // progressive sums belong to the scene they were rendered from: a new
     // scene restarts them (rtow_render_progressive)

@@ -24,6 +24,7 @@ namespace rtow_dev {
 enum : uint32_t {
     DK_BVH = 0,
     DK_SPHERE = 1,
+    DK_MSPHERE = 2,  // a sphere leaf reached through a general DNode's box slot (not inlined: time0/time1 not 0/1)
     DK_RECT = 3,
     DK_LIST = 4,
     DK_TRANSLATE = 5,
@@ -52,6 +53,10 @@ struct alignas(16) DBvh {  // 64 B
 // inner child (box min xyz, max xyz, 0, ref DK_BVH) or the sphere leaf itself
 // (center0 xyz, radius, center1 - center0 xyz, ref DK_SPHERE | sphere index),
 // so one node fetch carries everything a step needs.  Empty: ref DK_NONE.
+// General scenes (SAH mode, DevScene::gnode) use the same record as the twin
+// of every DBvh (same index): a sphere child with time0 = 0, time1 = 1 is
+// inlined, any other child is a box slot whose ref is the child (a
+// non-inlined sphere as DK_MSPHERE).
 struct alignas(16) DNode {
     float a[7];
     uint32_t ref_a;
@@ -122,12 +127,14 @@ struct alignas(16) DMedium {  // 32 B, constantMedium.h:21-23
 // descriptors are read with uniform (scalar) loads and the wave stays
 // together.  An item that is a chain of instances over one sphere, one
 // rectangle or a Box's rectangles is tested in place (the leaf's chain gives
-// the ray in the leaf's frame); anything else (media too) goes to the
-// general traversal.
-enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2 };
+// the ray in the leaf's frame); a medium whose boundary is a sphere or a
+// Box's rectangles (MB_SPHERE / MB_RECTS) is asked right there (TOP_MEDIUM,
+// with the closest hit so far as its tmax, hitableList.h:30); anything else
+// goes to the general traversal.
+enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2, TOP_MEDIUM = 3 };
 struct alignas(16) DTop {  // 16 B
     uint32_t kind;
-    uint32_t a;      // GENERIC: item ref; RECTS: first rectangle; SPHERE: sphere
+    uint32_t a;      // GENERIC: item ref; RECTS: first rectangle; SPHERE: sphere; MEDIUM: medium
     uint32_t b;      // RECTS: count
     uint32_t chain;  // the chain of the leaf's frame (GENERIC: of the list's frame)
 };
@@ -184,6 +191,7 @@ struct DevScene {
     uint32_t stack_need;     // deepest traversal stack a ray can need
     uint32_t has_media;
     uint32_t media_any;      // some medium's boundary needs the general traversal (MB_ANY)
+    uint32_t media_nested;   // some medium is not a top-level TOP_MEDIUM item
     // "simple" worlds: a chain of instances at the root, then only BvhNodes
     // and spheres (the random scene) -- traversed by the BVH-only kernel
     uint32_t simple;
@@ -192,6 +200,7 @@ struct DevScene {
     uint32_t root_chain[4];
     uint32_t bvh_root;       // root below the chain
     uint32_t n_node;         // DNode count (simple scenes)
+    uint32_t gnode;          // general scene: node[i] is the DNode twin of bvh[i] (DK_BVH steps read it)
 };
 
 }  // namespace rtow_dev
