@@ -174,7 +174,10 @@ typedef struct rtow_camera {
  * rank r of `world` renders tiles r, r+world, r+2*world, ... (the reference's
  * column interleave main.cpp:936, done by tiles). */
 enum {
-    RTOW_FLAG_STATS = 1u << 0 /* count segments (color() calls) on device */
+    RTOW_FLAG_STATS = 1u << 0,     /* count segments (color() calls) on device */
+    RTOW_FLAG_CAMERA_DOF = 1u << 1 /* CAMERA_DOF_EN 1 (defines.h:26; off in the reference's
+                                      build): Camera::getRay's offset is _lensRadius *
+                                      randomInUnitDisk() + randomInUnitSphere() (camera.h:124-126) */
 };
 
 typedef struct rtow_params {

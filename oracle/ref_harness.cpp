@@ -84,6 +84,12 @@ namespace std { using cbrng_engine = ::CbEngine; }
 #define private public
 #define protected public
 #include "defines.h"
+#ifdef RTOW_HARNESS_DOF
+// the ref_harness_dof build: camera.h:124-126 compiled with CAMERA_DOF_EN 1
+// (defines.h is #pragma once, so this value is the one camera.h sees)
+#undef CAMERA_DOF_EN
+#define CAMERA_DOF_EN 1
+#endif
 #include "vec3.h"
 #include "scenes.h"
 #undef private
@@ -189,6 +195,28 @@ static Hitable* threeSphereNed() {
     return new HitableList(list, 3);
 }
 
+// Not a reference scene: ConstantMedium below a BvhNode (the reference allows
+// it; its draws then follow BvhNode::hit's exhaustive both-children visit,
+// bvhNode.h:66-96, with the caller's interval, and an n == 1 node calls its
+// one leaf twice, bvhNode.h:38-39).  Built from the reference's classes in
+// the frame of threeSphereNed (camera at the origin looking along +x).
+static Hitable* mediumBvhNed() {
+    Texture* white = new ConstantTexture(vec3(0.9, 0.9, 0.9));
+    Texture* teal = new ConstantTexture(vec3(0.2, 0.8, 0.7));
+    Hitable** items = new Hitable*[6];
+    items[0] = new Sphere(vec3(10, 0, 0), 1, new Lambertian(new ConstantTexture(vec3(0.1, 0.2, 0.5))));
+    items[1] = new ConstantMedium(new Sphere(vec3(10, -2.2, 0), 1, new Dielectric(1.5)), 0.8f, white);
+    items[2] = new ConstantMedium(new Box(vec3(8, 1.5, -1), vec3(9.5, 3, 1), new Lambertian(white)), 0.5f, teal);
+    items[3] = new Sphere(vec3(10, 2.2, -1.6), 0.5, new Metal(vec3(0.8, 0.8, 0.9), 0.1));
+    items[4] = new ConstantMedium(new Sphere(vec3(12, 0, -2.5), 1.2, new Dielectric(1.5)), 0.3f, teal);
+    items[5] = new ConstantMedium(new Sphere(vec3(9, -0.9, -1.3), 0.4, new Dielectric(1.5)), 2.0f, white);
+    Hitable** list = new Hitable*[3];
+    list[0] = new Sphere(vec3(10, 0, 101), 100, new Lambertian(new ConstantTexture(vec3(0.8, 0.8, 0.0))));
+    list[1] = new BvhNode(items, 6, 0.0f, 1.0f);
+    list[2] = new Sphere(vec3(7, 0.5, -4), 0.6, new DiffuseLight(new ConstantTexture(vec3(4, 4, 4))));
+    return new HitableList(list, 3);
+}
+
 // Config 4: cornellBox_NED() with the smoke box that scenes.h:461-470 keeps
 // commented out, inserted at the position that code occupies (after the
 // rotated box, before the sphere medium).
@@ -289,6 +317,7 @@ static Hitable* buildWorld(const std::string& name, const Opts& o) {
     if (name == "cornell") return new Translate(cornellBox_NED(), vec3(800, 0, 0));
     if (name == "cornell_smoke") return new Translate(cornellSmokeNed(), vec3(800, 0, 0));
     if (name == "three_sphere") return threeSphereNed();
+    if (name == "medium_bvh") return mediumBvhNed();
     if (name == "final_ned") {
         bool used;
         return new Translate(finalSceneNed(&used), vec3(600, -278, 278));

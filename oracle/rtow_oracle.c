@@ -64,6 +64,18 @@ typedef struct {
     uint32_t mat;
 } hitrec;
 
+/* mathUtilities.h:11-17: 2.0*vec3(U, U, 0) - vec3(1,1,0), the constructor's
+ * arguments evaluated right to left (y drawn first) */
+static v3 random_in_unit_disk(ctx_t* cx, rng_t* g) {
+    v3 p;
+    do {
+        double b = unif(cx, g);
+        double a = unif(cx, g);
+        p = sub(scl(2.0f, mk((float)a, (float)b, 0.0f)), mk(1, 1, 0));
+    } while (dot(p, p) >= 1.0);
+    return p;
+}
+
 /* mathUtilities.h:19-25 */
 static v3 random_in_unit_sphere(ctx_t* cx, rng_t* g) {
     v3 p;
@@ -541,9 +553,20 @@ static v3 sample_color(ctx_t* cx, const rtow_camera* C, const rtow_params* P, in
         uint64_t d0 = cx->c.draws;
         float u = (float)(column + unif(cx, &g)) / (float)W;
         float v = (float)(row + unif(cx, &g)) / (float)H;
-        /* camera.h:123-135 with CAMERA_DOF_EN 0 */
+        /* camera.h:123-135: CAMERA_DOF_EN 0 (the reference default) or, with
+         * RTOW_FLAG_CAMERA_DOF, CAMERA_DOF_EN 1 */
         float lr = C->lens_radius;
-        v3 rd = scl(lr, mk(1.0f, 1.0f, 1.0f));
+        v3 rd;
+        if (P->flags & RTOW_FLAG_CAMERA_DOF) {
+            /* camera.h:125: _lensRadius * randomInUnitDisk() + randomInUnitSphere();
+             * g++ evaluates operator+'s arguments right to left: the sphere's
+             * draws come first (pinned by the ref_harness_dof fixtures) */
+            v3 sph = random_in_unit_sphere(cx, &g);
+            v3 disk = random_in_unit_disk(cx, &g);
+            rd = add(scl(lr, disk), sph);
+        } else {
+            rd = scl(lr, mk(1.0f, 1.0f, 1.0f));
+        }
         v3 offset = add(scl(rd.x, ld3(C->u)), scl(rd.y, ld3(C->v)));
         float time = (float)(C->time0 + unif(cx, &g) * (double)(C->time1 - C->time0));
         ray_t r;

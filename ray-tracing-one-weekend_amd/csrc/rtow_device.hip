@@ -116,6 +116,7 @@ struct DevParams {
     uint32_t n_chunks, n_local_px, tiles_x, rank, world;
     uint32_t n_big, tail_r, n_tail;
     uint32_t max_depth, gi_enable;
+    uint32_t dof;  // RTOW_FLAG_CAMERA_DOF: camera.h:124-126 with CAMERA_DOF_EN 1
     float sky_gain, gi_gain;
     uint64_t seed;
     uint32_t n_items;
@@ -390,6 +391,22 @@ __device__ __forceinline__ bool ref_aabb_hit(const float* b, const Ray& r, float
     const float4 lo = *(const float4*)b, hi = *(const float4*)(b + 4);
     return ref_slab(lo.x, hi.x, r.o.x, r.d.x, tmin, tmax) && ref_slab(lo.y, hi.y, r.o.y, r.d.y, tmin, tmax) &&
            ref_slab(lo.z, hi.z, r.o.z, r.d.z, tmin, tmax);
+}
+
+// The same with the ray's IEEE reciprocals: (x - o) / d as div_by_any gives
+// it (the correctly rounded quotient; +-inf and NaN where d is zero)
+__device__ __forceinline__ bool ref_slab_inv(float mn, float mx, float o, float d, float rd, float& tmin, float& tmax) {
+    const float p = div_by_any(mn - o, d, rd), q = div_by_any(mx - o, d, rd);
+    const float t0 = p < q ? p : q, t1 = p > q ? p : q;
+    tmin = t0 > tmin ? t0 : tmin;
+    tmax = t1 < tmax ? t1 : tmax;
+    return !(tmax <= tmin);
+}
+__device__ __forceinline__ bool ref_aabb_hit_inv(const float* b, const Ray& r, const F3& inv, float tmin, float tmax) {
+    const float4 lo = *(const float4*)b, hi = *(const float4*)(b + 4);
+    return ref_slab_inv(lo.x, hi.x, r.o.x, r.d.x, inv.x, tmin, tmax) &&
+           ref_slab_inv(lo.y, hi.y, r.o.y, r.d.y, inv.y, tmin, tmax) &&
+           ref_slab_inv(lo.z, hi.z, r.o.z, r.d.z, inv.z, tmin, tmax);
 }
 
 // Does the reference test rectangle `rect` for this ray at all?  BvhNode::hit
@@ -791,6 +808,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
     float a = dot(r.d, r.d);
     float ra = 1.0f / a;
     float bt = tmax;
+    float tmed = __builtin_nanf("");  // a DProg medium's interval end (NaN: none pending)
     bool found = false;
     best.prim = prev;
     uint32_t cur = root;
@@ -886,9 +904,55 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
             q = slab_ray(r);
             a = dot(r.d, r.d);
             ra = 1.0f / a;
+        } else if (kind == DK_PROG || kind == DK_PROGNEXT) {
+            if constexpr (MEDIA) {
+                // a BvhNode subtree holding media, replayed in the reference's
+                // visit order (DProg); tin: the end of the interval the
+                // subtree was handed, which every box and medium in it sees
+                uint32_t pos = idx;
+                float tin = bt;
+                if (kind == DK_PROGNEXT) {  // back from an item: its interval sits below the marker
+                    --sp;
+                    tin = __uint_as_float(stk[sp * BLOCK]);
+                }
+                bool descend = false;
+                while (true) {
+                    const DProg* E = S.prog + pos;
+                    const uint4 w = reinterpret_cast<const uint4*>(E)[1];
+                    const uint32_t op = __float_as_uint(reinterpret_cast<const float4*>(E)[0].w);
+                    if (op == PROG_END) break;
+                    if (op == PROG_BOX) {
+                        pos += ref_aabb_hit_inv(reinterpret_cast<const float*>(E), r, q.inv, tmin, tin) ? 1u : 1u + w.w;
+                        continue;
+                    }
+                    // an item: a medium (asked with the subtree's interval,
+                    // below) or a child without media (the general traversal:
+                    // nearest hit and exact ties merge as anywhere else);
+                    // then on with the program
+                    pos++;
+                    if (sp + 2 <= STACK) {
+                        stk[sp * BLOCK] = __float_as_uint(tin);
+                        stk[(sp + 1) * BLOCK] = mkref(DK_PROGNEXT, pos);
+                        sp += 2;
+                        cur = w.w;
+                        if ((cur >> KIND_SHIFT) == DK_MEDIUM) tmed = tin;
+                        descend = true;
+                    } else {
+                        overflow = 1;
+                    }
+                    break;
+                }
+                if (descend) continue;
+            }
         } else if (kind == DK_MEDIUM) {
             if constexpr (MEDIA) {
-                if (medium_hit<STACK, ANYB>(S, idx, r, a, wray, tmin, bt, stk, sp, rng, overflow)) {
+                // asked with the closest hit so far, or (tmed, set by a DProg
+                // program) its subtree's interval; the nearest record is kept
+                float tm = tmed == tmed ? tmed : bt;
+                tmed = __builtin_nanf("");
+                if (medium_hit<STACK, ANYB>(S, idx, r, a, wray, tmin, tm, stk, sp, rng, overflow) &&
+                    (tm < bt || (tm == bt && wins_tie(S, cur, best.prim)))) {
+                    bt = tm;
                     best.prim = cur;
                     found = true;
                 }
@@ -908,7 +972,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
 // MEDIA / ANYB: media below the top level (the general traversal asks them);
 // TOPMED: media as top-level items (TOP_MEDIUM).
 template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false>
-__device__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
+__device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
                              uint32_t& overflow, bool strict, Prof* prof = nullptr) {
     float bt = FLT_MAX;
     uint32_t bp = mkref(DK_NONE, 0);
@@ -1294,8 +1358,22 @@ __device__ __forceinline__ bool decode_pixel(const DevParams& P, uint32_t lp, ui
     return x < P.width && yimg < P.height;
 }
 
-// main.cpp:943-946 + camera.h:123-135 (CAMERA_DOF_EN 0): the sample's jitter,
-// time and primary ray; the counter restarts per sample
+// mathUtilities.h:11-17: 2.0*vec3(U, U, 0) - vec3(1,1,0) until inside the unit
+// disk; the constructor's arguments are evaluated right to left (y first)
+__device__ __forceinline__ F3 random_in_unit_disk(Rng& g) {
+    F3 p;
+    do {
+        const float b = g.nextf();
+        const float a = g.nextf();
+        p = sub(scl(2.0f, f3(a, b, 0.0f)), f3(1, 1, 0));
+    } while (dot(p, p) >= 1.0f);
+    return p;
+}
+// main.cpp:943-946 + camera.h:123-135: the sample's jitter, time and primary
+// ray; the counter restarts per sample.  CAMERA_DOF_EN 0 (the reference's
+// build) or, with P.dof, 1: the lens offset draws a unit-sphere point, then a
+// unit-disk point (the order g++ evaluates operator+'s arguments in; the
+// ref_harness_dof fixtures pin it)
 __device__ __forceinline__ void camera_ray(const DevCam& C, const DevParams& P, uint32_t col, uint32_t row,
                                           uint32_t s, Rng& rng, Ray& ray) {
     rng.key = rtow_sample_key(P.seed, row * P.width + col, P.sample_base + s);
@@ -1304,7 +1382,11 @@ __device__ __forceinline__ void camera_ray(const DevCam& C, const DevParams& P, 
     // float rounding is the float sum's (makeParams bounds W and H by 2^24)
     const float u = ((float)col + rng.nextf()) / (float)P.width;
     const float v = ((float)row + rng.nextf()) / (float)P.height;
-    const F3 rd = scl(C.lens_radius, f3(1.0f, 1.0f, 1.0f));
+    F3 rd = scl(C.lens_radius, f3(1.0f, 1.0f, 1.0f));
+    if (P.dof) {
+        const F3 sph = random_in_unit_sphere(rng);
+        rd = add(scl(C.lens_radius, random_in_unit_disk(rng)), sph);
+    }
     const F3 offset = add(scl(rd.x, ld3(C.u)), scl(rd.y, ld3(C.v)));
     // with t0 == 0 the double expression is the exact product U*(t1-t0)
     // rounded once to float, as the float product is (0.0f + keeps -0 -> +0)
@@ -1786,6 +1868,7 @@ struct HostLayout {
     std::unordered_map<uint32_t, uint32_t> collapsed_of;
     std::vector<uint32_t> rect_anc;  // DevScene::rect_anc
     std::vector<float> abox;         // DevScene::abox
+    std::vector<DProg> prog;         // DevScene::prog
 };
 
 // ---------------------------------------------------------------------------
@@ -2138,33 +2221,35 @@ uint32_t sahBuildBvh(std::vector<GenLeaf>& P, size_t lo, size_t hi, std::vector<
     return mkref(DK_BVH, idx);
 }
 
+// Does anything below `ref` draw random numbers during traversal?
+bool refHasMedium(const HostLayout& L, uint32_t ref, int depth = 0) {
+    const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+    if (depth > 512) return true;
+    switch (kind) {
+    case DK_MEDIUM:
+        return true;
+    case DK_BVH:
+        return refHasMedium(L, L.bvh[idx].left, depth + 1) || refHasMedium(L, L.bvh[idx].right, depth + 1);
+    case DK_LIST: {
+        const DList& l = L.list[idx];
+        for (uint32_t j = 0; j < l.count; j++)
+            if (refHasMedium(L, L.refs[l.first + j], depth + 1)) return true;
+        return false;
+    }
+    case DK_TRANSLATE:
+    case DK_ROTY:
+    case DK_FLIP:
+        return refHasMedium(L, L.inst[idx].child, depth + 1);
+    default:
+        return false;
+    }
+}
+
 struct GeneralSah {
     HostLayout& L;
     uint32_t n_old;  // DBvh nodes of the reference trees (new ones come after)
 
-    // Does anything below `ref` draw random numbers during traversal?
-    bool hasMedium(uint32_t ref, int depth = 0) const {
-        const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
-        if (depth > 512) return true;
-        switch (kind) {
-        case DK_MEDIUM:
-            return true;
-        case DK_BVH:
-            return hasMedium(L.bvh[idx].left, depth + 1) || hasMedium(L.bvh[idx].right, depth + 1);
-        case DK_LIST: {
-            const DList& l = L.list[idx];
-            for (uint32_t j = 0; j < l.count; j++)
-                if (hasMedium(L.refs[l.first + j], depth + 1)) return true;
-            return false;
-        }
-        case DK_TRANSLATE:
-        case DK_ROTY:
-        case DK_FLIP:
-            return hasMedium(L.inst[idx].child, depth + 1);
-        default:
-            return false;
-        }
-    }
+    bool hasMedium(uint32_t ref) const { return refHasMedium(L, ref); }
 
     // A box holding every hit point of `ref`, in the frame `ref` sits in
     // (false: unbounded).  Only used to cull, so it is padded well beyond the
@@ -2580,11 +2665,7 @@ struct Converter {
             break;
         }
         case RTOW_HIT_CONSTANT_MEDIUM: {
-            if (underBvh) {
-                err = "ConstantMedium below a BvhNode: its random draws follow the reference's exhaustive "
-                      "BVH visit order, which the device traversal does not reproduce";
-                return mkref(DK_NONE, 0);
-            }
+            (void)underBvh;  // below a BvhNode: replayed in the reference's visit order (ProgramBuilder)
             L.has_media = true;
             uint32_t slot = (uint32_t)L.med.size();
             L.med.push_back(DMedium{});
@@ -2643,6 +2724,15 @@ struct Bounds {
             r = c;
             break;
         }
+        case DK_PROG:  // a medium is asked in place; any other item below a continuation (2 entries)
+            for (uint32_t p = idx; p < L.prog.size() && L.prog[p].op != PROG_END; p++) {
+                if (L.prog[p].op != PROG_ITEM) continue;
+                const uint32_t it = L.prog[p].arg;
+                auto c = need(it, inMedium);
+                const uint32_t cont = (it >> KIND_SHIFT) == DK_MEDIUM ? 0u : 2u;
+                r = {std::max(r.first, cont + c.first), std::max(r.second, c.second)};
+            }
+            break;
         default:
             break;
         }
@@ -2712,6 +2802,102 @@ void refAncestors(HostLayout& L, uint32_t ref, std::vector<uint32_t>& path, int 
     }
     if (collapsed) path.pop_back();
 }
+
+// BvhNode subtrees that hold media become DProg programs (DK_PROG): the
+// reference's own BvhNode boxes (bvhNode.h:58; an n == 1 node's too) in
+// depth-first order, each with how many entries its children take, the
+// media as items called with the subtree's interval, every medium-free child
+// as one item for the general traversal.  Run after the tie keys, the
+// rectangles' ancestor boxes and the SAH rebuild (none of which touch a
+// subtree with media) on the reference graph.
+struct ProgramBuilder {
+    HostLayout& L;
+    std::string err;
+
+    void box(const float* o, std::vector<DProg>& P) {
+        DProg e{};
+        for (int a = 0; a < 3; a++) {
+            e.lo[a] = o[a];
+            e.hi[a] = o[3 + a];
+        }
+        e.op = PROG_BOX;
+        P.push_back(e);
+    }
+    void item(uint32_t ref, std::vector<DProg>& P) {
+        DProg e{};
+        e.op = PROG_ITEM;
+        e.arg = ref;
+        P.push_back(e);
+    }
+    // a child of a BvhNode with media (or a subtree root): an n == 1 node
+    // (collapsed into its leaf by the converter) calls its leaf twice
+    void child(uint32_t ref, std::vector<DProg>& P, int depth) {
+        const auto col = L.collapsed_of.find(ref);
+        if (col != L.collapsed_of.end() && refHasMedium(L, ref)) {
+            const size_t at = P.size();
+            box(&L.collapsed_own[6 * (size_t)col->second], P);
+            node(ref, P, depth + 1);
+            node(ref, P, depth + 1);
+            P[at].arg = (uint32_t)(P.size() - at - 1);
+            return;
+        }
+        node(ref, P, depth + 1);
+    }
+    void node(uint32_t ref, std::vector<DProg>& P, int depth) {
+        if (depth > 512) {
+            err = "BvhNode subtree with media too deep";
+            return;
+        }
+        const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+        if (kind == DK_BVH && refHasMedium(L, ref)) {
+            if (6 * (size_t)idx + 6 > L.bvh_own.size()) {
+                err = "BvhNode with media without its own box";
+                return;
+            }
+            const size_t at = P.size();
+            box(&L.bvh_own[6 * (size_t)idx], P);
+            child(L.bvh[idx].left, P, depth);
+            child(L.bvh[idx].right, P, depth);
+            P[at].arg = (uint32_t)(P.size() - at - 1);
+        } else if (kind == DK_MEDIUM || !refHasMedium(L, ref)) {
+            item(ref, P);
+        } else {
+            // an instance or list with media below a BvhNode would hand its
+            // media the list's shrinking interval / its own frame: not replayed
+            err = "ConstantMedium below a BvhNode behind an instance or a list";
+        }
+    }
+    void patch(uint32_t& ref, int depth = 0) {
+        if (depth > 512 || !err.empty()) return;
+        const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+        const bool n1 = L.collapsed_of.count(ref) != 0;
+        if ((kind == DK_BVH || n1) && refHasMedium(L, ref)) {
+            const uint32_t start = (uint32_t)L.prog.size();
+            std::vector<DProg> P;
+            child(ref, P, 0);
+            DProg end{};
+            end.op = PROG_END;
+            P.push_back(end);
+            L.prog.insert(L.prog.end(), P.begin(), P.end());
+            ref = mkref(DK_PROG, start);
+            return;
+        }
+        switch (kind) {
+        case DK_LIST: {
+            const DList l = L.list[idx];
+            for (uint32_t j = 0; j < l.count; j++) patch(L.refs[l.first + j], depth + 1);
+            break;
+        }
+        case DK_TRANSLATE:
+        case DK_ROTY:
+        case DK_FLIP:
+            patch(L.inst[idx].child, depth + 1);
+            break;
+        default:
+            break;
+        }
+    }
+};
 
 // DTop descriptors of a general scene whose root, below its instances, is a
 // list (empty otherwise)
@@ -2945,6 +3131,15 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         Bounds bd2{L};
         L.stack_need = bd2.need(L.root, false).first;
     }
+    if (!L.simple) {  // BvhNode subtrees with media: replayed programs (DK_PROG)
+        ProgramBuilder pb{L};
+        pb.patch(L.root);
+        if (!pb.err.empty()) return set_error(RTOW_E_UNSUPPORTED, pb.err);
+        if (!L.prog.empty()) {
+            Bounds bd3{L};
+            L.stack_need = bd3.need(L.root, false).first;
+        }
+    }
     // how each medium's boundary is queried (DMedium::bkind); REFERENCE mode
     // keeps the general traversal for all of them
     for (DMedium& M : L.med) {
@@ -3166,6 +3361,7 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     P.n_items = (uint32_t)items;
     P.max_depth = p->max_depth;
     P.gi_enable = p->gi_enable;
+    P.dof = (p->flags & RTOW_FLAG_CAMERA_DOF) ? 1u : 0u;
     P.sky_gain = p->sky_gain;
     P.gi_gain = p->gi_gain;
     P.seed = p->seed;
@@ -3395,6 +3591,8 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     if (L.rect_anc.empty()) L.rect_anc.push_back(0u);
     if (L.abox.empty()) L.abox.assign(8, 0.0f);
     size_t o_anc = pushBlob(blob, L.rect_anc), o_abox = pushBlob(blob, L.abox);
+    if (L.prog.empty()) L.prog.push_back(DProg{});
+    size_t o_prog = pushBlob(blob, L.prog);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -3428,6 +3626,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.n_top = (uint32_t)L.top.size();
     d.rect_anc = (const uint32_t*)(b + o_anc);
     d.abox = (const float*)(b + o_abox);
+    d.prog = (const DProg*)(b + o_prog);
     d.root = L.root;
     d.stack_need = L.stack_need;
     d.has_media = L.has_media ? 1u : 0u;

@@ -34,6 +34,8 @@ enum : uint32_t {
     DK_EXIT = 9,  // traversal-stack marker: leave the innermost instance
     DK_LISTNEXT = 10,  // traversal-stack marker: continue a list at refs[index]
     DK_RECTS = 11,     // a list of rectangles only (a Box's sides): DList over rect[first, first+count)
+    DK_PROG = 12,      // a BvhNode subtree holding media, visited as the reference visits it (DProg)
+    DK_PROGNEXT = 13,  // traversal-stack marker: continue a DProg program at prog[index]
     DK_NONE = 15
 };
 
@@ -122,6 +124,28 @@ struct alignas(16) DMedium {  // 32 B, constantMedium.h:21-23
     uint32_t bkind, bfirst, bcount, bchain;
 };
 
+// A BvhNode subtree with ConstantMedium leaves.  BvhNode::hit (bvhNode.h:66-96)
+// tests its own box (AABB::hit, aabb.h:22-43) with the interval it was handed
+// and then BOTH children with that same interval; a medium draws a number on
+// every call (constantMedium.h:27, a second one when the ray crosses its
+// boundary), so which media are called, how often and in what order is the
+// reference's exhaustive depth-first visit -- the device replays it as a
+// flat program, one entry per step:
+//   PROG_BOX  the node's own box (lo, hi); when AABB::hit fails, skip the
+//             `arg` entries of its children's programs;
+//   PROG_ITEM `arg` is a child the visit order does not matter for (no media
+//             below it: its closest hit merges by the tie keys) or a medium,
+//             called with the subtree's interval;
+//   PROG_END  the end of the program.
+// An n == 1 node (bvhNode.h:38-39) calls its one leaf twice: two ITEMs.
+enum : uint32_t { PROG_BOX = 0, PROG_ITEM = 1, PROG_END = 2 };
+struct alignas(16) DProg {  // 32 B; lo/hi read as ref_aabb_hit's (min xyz, -, max xyz, -)
+    float lo[3];
+    uint32_t op;
+    float hi[3];
+    uint32_t arg;
+};
+
 // The top-level list of a general scene (below the root's instances), as the
 // kernel scans it: item by item with the whole wave on the same item, so the
 // descriptors are read with uniform (scalar) loads and the wave stays
@@ -168,6 +192,7 @@ struct DevScene {
     const DMedium* med;
     const DChain* chains;
     const DTop* top;         // general scenes: the top-level list, n_top items (0: none)
+    const DProg* prog;       // programs of the BvhNode subtrees that hold media (DK_PROG)
     uint32_t n_top;
     // Per rectangle: (offset << 8) | count of the boxes (8 floats each in
     // abox: min xyz, 0, max xyz, 0) of the reference BvhNodes above it in its

@@ -191,6 +191,10 @@ def check(rc, where):
         raise RtowError(rc, where, f"{L.rtow_error_string(rc).decode()}: {L.rtow_last_error().decode()}")
 
 
+FLAG_STATS = 1 << 0
+FLAG_CAMERA_DOF = 1 << 1  # CAMERA_DOF_EN 1 (camera.h:124-126)
+
+
 def params(width, height, spp, seed=1, **kw):
     p = Params()
     lib().rtow_params_default(ctypes.byref(p), width, height, spp)

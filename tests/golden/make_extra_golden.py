@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Golden fixtures beyond the BASELINE configs, from the REFERENCE ITSELF
+(oracle/_ref, the reference's headers unmodified):
+
+* dof_*: the depth-of-field camera path (RTOW_FLAG_CAMERA_DOF), rendered by
+  oracle/_ref/ref_harness_dof -- the same harness as make_golden.py's,
+  compiled with CAMERA_DOF_EN 1 (camera.h:124-126);
+* medium_bvh: ConstantMedium below a BvhNode (ref_harness.cpp mediumBvhNed:
+  the reference's classes, media in the BVH, one in an n == 1 node).
+
+Writes <case>.{scn,lin,bgra} (texels stripped, as make_golden.py), the
+cameras, and manifest_extra.json (`flags`: the rtow_params flags the case
+renders with).
+
+Usage: python3 tests/golden/make_extra_golden.py   (after make -C oracle ref)
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+HARNESS_DOF = os.path.join(REPO, "oracle", "_ref", "ref_harness_dof")
+
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+from make_golden import strip_texels, write_png  # noqa: E402
+from scene_io import synthetic_image  # noqa: E402
+
+FLAG_CAMERA_DOF = 2  # include/rtow.h
+# name, harness, flags, harness scene, n, image mode, W, H, spp, render seed
+CASES = [
+    ("dof_three_sphere", HARNESS_DOF, FLAG_CAMERA_DOF, "three_sphere", 100, "none", 64, 36, 16, 3),
+    ("dof_random100", HARNESS_DOF, FLAG_CAMERA_DOF, "random_ned", 100, "synthetic", 48, 27, 16, 5),
+    ("medium_bvh", HARNESS, 0, "medium_bvh", 100, "none", 64, 36, 64, 9),
+]
+SCENE_SEED = 1
+
+
+def main():
+    if not (os.path.exists(HARNESS) and os.path.exists(HARNESS_DOF)):
+        sys.exit("build the harnesses first: make -C oracle ref")
+    tmp = tempfile.mkdtemp(prefix="rtow_dof_")
+    dirs = {"none": os.path.join(tmp, "none"), "synthetic": os.path.join(tmp, "synth")}
+    os.makedirs(dirs["none"])
+    os.makedirs(os.path.join(dirs["synthetic"], "input_images"))
+    write_png(os.path.join(dirs["synthetic"], "input_images", "1_earth_8k.jpg"), synthetic_image(2048, 1024))
+    env = dict(os.environ, RTOW_SCENE_SEED=str(SCENE_SEED))
+    manifest = {"scene_seed": SCENE_SEED, "generator": "oracle/_ref/ref_harness[_dof]", "cases": []}
+    for name, harness, flags, scene, n, img, W, H, spp, seed in CASES:
+        raw = os.path.join(tmp, name + ".scn")
+        subprocess.run([harness, "dump", scene, raw, "--n", str(n), "--cwd", dirs[img]], env=env, check=True,
+                       capture_output=True)
+        sha, ntex, hdr = strip_texels(raw, os.path.join(HERE, name + ".scn"))
+        subprocess.run([harness, "render", scene, str(W), str(H), str(spp), os.path.join(HERE, name),
+                        "--n", str(n), "--seed", str(seed), "--cwd", dirs[img]], env=env, check=True)
+        subprocess.run([HARNESS, "camera", str(W), str(H), os.path.join(HERE, f"cam_{W}x{H}.cam")], env=env,
+                       check=True)
+        manifest["cases"].append(dict(name=name, harness=os.path.basename(harness), flags=flags, scene=scene, n=n, image=img, width=W, height=H, spp=spp, seed=seed,
+                                      texel_bytes=ntex, texel_sha256=sha, n_hitables=hdr[2]))
+        print(f"{name}: {hdr[2]} hitables")
+    with open(os.path.join(HERE, "manifest_extra.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

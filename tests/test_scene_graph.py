@@ -63,28 +63,47 @@ def test_scene_check_bounds():
     assert st <= 64 and ch == 3  # Translate(root) > Translate > RotateY; FlipNormals folds into its rectangle
 
 
-def test_medium_under_bvh_rejected(tmp_path):
-    """A ConstantMedium below a BvhNode draws random numbers in the
-    reference's exhaustive visit order; the device path refuses it loudly."""
+def _medium_under_bvh(tmp_path, behind_translate):
     s = rtow.Scene.build("random_ned", n=100)
     d = sio.load_scene(_save(s, tmp_path))
     h = d["hitables"]
     idx = int(np.nonzero(h["kind"] == 1)[0][-1])  # some sphere under the BVH
-    med = np.zeros(1, sio.HITABLE)
-    med[0]["kind"] = 12
-    med[0]["a"] = idx
-    med[0]["b"] = 0
-    med[0]["f"][0] = 0.5
-    d["hitables"] = np.concatenate([h, med])
-    # re-point a BVH child at the medium
-    bvh = int(np.nonzero(d["hitables"]["kind"] == 11)[0][-1])
-    d["hitables"][bvh]["a"] = len(h)
-    arr = sio.SceneArrays(d)
+    extra = np.zeros(3 if behind_translate else 2, sio.HITABLE)
+    extra[0] = h[idx]  # the boundary: a copy of that sphere
+    extra[1]["kind"] = 12  # ConstantMedium(sphere, density 0.5, phase material 0)
+    extra[1]["a"] = len(h)
+    extra[1]["b"] = 0
+    extra[1]["f"][0] = 0.5
+    target = len(h) + 1
+    if behind_translate:
+        extra[2]["kind"] = sio.HIT_TRANSLATE
+        extra[2]["a"] = len(h) + 1
+        extra[2]["f"][:3] = (0.0, 1.0, 0.0)
+        target = len(h) + 2
+    d["hitables"] = np.concatenate([h, extra])
+    bvh = int(np.nonzero(d["hitables"]["kind"] == 11)[0][-1])  # re-point a BVH child
+    d["hitables"][bvh]["a"] = target
+    return sio.SceneArrays(d)
+
+
+def test_medium_under_bvh_accepted(tmp_path):
+    """A ConstantMedium below a BvhNode is replayed in the reference's
+    exhaustive visit order (DProg; GPU parity: tests/test_medium_bvh.py)."""
     import ctypes
 
+    arr = _medium_under_bvh(tmp_path, False)
+    assert rtow.lib().rtow_scene_check(ctypes.addressof(arr.view), None, None) == rtow.OK
+
+
+def test_medium_under_bvh_behind_instance_rejected(tmp_path):
+    """...but not behind an instance or list there (the interval and frame the
+    medium would see are not replayed): refused loudly."""
+    import ctypes
+
+    arr = _medium_under_bvh(tmp_path, True)
     rc = rtow.lib().rtow_scene_check(ctypes.addressof(arr.view), None, None)
     assert rc == rtow.E_UNSUPPORTED
-    assert b"BvhNode" in rtow.lib().rtow_last_error()
+    assert b"instance or a list" in rtow.lib().rtow_last_error()
 
 
 def _save(s, tmp_path):
