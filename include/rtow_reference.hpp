@@ -9,6 +9,8 @@
  *   rtow_scene_upload(ctx, w.view());    // include/rtow.h
  *   rtow_camera cam;
  *   rtow_ref::camera(mainCamera, &cam);  // the basis Camera::getRay reads
+ *   rtow_params params;
+ *   rtow_ref::params(W, H, spp, &params);  // defines.h of this build (DOF, GI gains, depth)
  *   rtow_render(ctx, &cam, &params, bgra, nullptr, &stats);
  *
  * World walks the object graph depth first in the canonical order
@@ -288,6 +290,29 @@ inline int camera(Camera& c, rtow_camera* out) {
     out->time0 = t0;
     out->time1 = t1;
     return RTOW_OK;
+}
+
+/* The render parameters of THIS build of the reference: defines.h as the
+ * translation unit sees it (GLOBAL_ILLUM_EN, SKY_ILLUM_GAIN,
+ * GLOBAL_ILLUM_GAIN, DEPTH_RECURSION, CAMERA_DOF_EN -> RTOW_FLAG_CAMERA_DOF),
+ * over rtow_params_default's values for anything defines.h leaves out. */
+inline void params(uint32_t width, uint32_t height, uint32_t spp, rtow_params* out) {
+    rtow_params_default(out, width, height, spp);
+#ifdef GLOBAL_ILLUM_EN
+    out->gi_enable = GLOBAL_ILLUM_EN ? 1u : 0u;
+#endif
+#ifdef SKY_ILLUM_GAIN
+    out->sky_gain = (float)SKY_ILLUM_GAIN;
+#endif
+#ifdef GLOBAL_ILLUM_GAIN
+    out->gi_gain = (float)GLOBAL_ILLUM_GAIN;
+#endif
+#ifdef DEPTH_RECURSION
+    out->max_depth = DEPTH_RECURSION;
+#endif
+#if defined(CAMERA_DOF_EN) && CAMERA_DOF_EN == 1
+    out->flags |= RTOW_FLAG_CAMERA_DOF;
+#endif
 }
 
 }  // namespace rtow_ref

@@ -576,7 +576,7 @@ int main(int argc, char** argv) {
         int rc2 = rtow_context_create(0, &ctx);
         if (rc2 == RTOW_OK) rc2 = rtow_scene_upload(ctx, w.view());
         rtow_params p;
-        rtow_params_default(&p, W, H, spp);
+        rtow_ref::params(W, H, spp, &p);  // this build's defines.h
         p.seed = o.seed;
         std::vector<uint8_t> bgra((size_t)W * H * 4);
         std::vector<float> lin((size_t)W * H * 3);
