@@ -230,7 +230,9 @@ enum {
 enum {
     RTOW_IMAGE_NONE = 0,       /* stbi_load failed: the reference's glass fallback */
     RTOW_IMAGE_SYNTHETIC = 1,  /* rtow_synthetic_image(2048, 1024) */
-    RTOW_IMAGE_RAW = 2         /* RGB8 raw file image_path, image_nx * image_ny * 3 */
+    RTOW_IMAGE_RAW = 2,        /* RGB8 raw file image_path, image_nx * image_ny * 3 */
+    RTOW_IMAGE_JPEG = 3        /* JPEG file image_path, decoded as stbi_load(path, .., 0) decodes it
+                                  (rtow_image_load_jpeg; scenes.h:140 loads 1_earth_8k.jpg) */
 };
 
 typedef struct rtow_build_opts {
@@ -261,6 +263,16 @@ int rtow_camera_main(uint32_t width, uint32_t height, rtow_camera* out);
  * as setCamera_QuaternionMatrix (camera.h:315-342) forms it. */
 int rtow_camera_oriented(uint32_t width, uint32_t height, const float look_from[3], const float rows[9],
                          rtow_camera* out);
+/* JPEG decoding as the reference's stb_image.h v2.22 does it (stbi_load with
+ * req_comp 0, scenes.h:140): baseline and progressive Huffman, 8-bit, 1/3/4
+ * components, any sampling, restart intervals; same bytes as stbi_load
+ * (tests/test_jpeg.py).  *pixels: nx * ny * channels bytes, row 0 first,
+ * channels 3 (or 1 for a grayscale file); free with rtow_image_free. */
+int rtow_image_decode_jpeg(const uint8_t* data, size_t size, uint8_t** pixels, uint32_t* nx, uint32_t* ny,
+                           uint32_t* channels);
+int rtow_image_load_jpeg(const char* path, uint8_t** pixels, uint32_t* nx, uint32_t* ny, uint32_t* channels);
+void rtow_image_free(uint8_t* pixels);
+
 /* Fill an RGB8 image with the synthetic "earth" stand-in. */
 void rtow_synthetic_image(uint32_t nx, uint32_t ny, uint8_t* rgb);
 

@@ -20,6 +20,7 @@
 // Usage:
 //   ref_harness dump   <scene> <out.scn> [opts]
 //   ref_harness camera <W> <H> <out.cam>
+//   ref_harness decode <file.jpg> <out.img>   (stbi_load(path, .., 0): u32 nx, ny, n + pixels)
 //   ref_harness camera_oriented <W> <H> <lookfrom xyz> <view xyz> <east xyz> <down xyz> <out.cam>
 //   ref_harness render <scene> <W> <H> <spp> <out_prefix> [opts]
 //   ref_harness bench  <scene> <W> <H> <spp> <pixels.u32> [opts]   (timing, JSON line)
@@ -472,6 +473,22 @@ int main(int argc, char** argv) {
         if (w.status() != RTOW_OK) { std::fprintf(stderr, "unknown object class\n"); return 3; }
         writeScene(argv[3], *w.view());
         std::printf("draws %llu hitables %u\n", (unsigned long long)CbEngine::total, w.view()->n_hitables);
+        return 0;
+    }
+    if (cmd == "decode" && argc >= 4) {
+        // the reference's own stb_image (scenes.h:26-27, stb_image.h v2.22)
+        // on a file, as scenes.h:140 calls it: uint32 nx, ny, channels, then
+        // the pixels (tests/golden/jpeg/make_jpeg_golden.py)
+        int x = 0, y = 0, n = 0;
+        unsigned char* px = stbi_load(argv[2], &x, &y, &n, 0);
+        if (!px) { std::fprintf(stderr, "stbi_load: %s\n", stbi_failure_reason()); return 5; }
+        FILE* f = std::fopen(argv[3], "wb");
+        if (!f) { std::perror(argv[3]); return 2; }
+        const uint32_t hdr[3] = {(uint32_t)x, (uint32_t)y, (uint32_t)n};
+        std::fwrite(hdr, 4, 3, f);
+        std::fwrite(px, 1, (size_t)x * y * n, f);
+        std::fclose(f);
+        stbi_image_free(px);
         return 0;
     }
     if (cmd == "camera" && argc >= 5) {

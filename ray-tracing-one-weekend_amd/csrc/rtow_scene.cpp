@@ -589,6 +589,23 @@ int buildWorld(int sceneId, const rtow_build_opts& o, World& out) {
         if (o.image_mode == RTOW_IMAGE_SYNTHETIC) {
             out.images.push_back(syntheticImage(2048, 1024));
             earth = &out.images.back();
+        } else if (o.image_mode == RTOW_IMAGE_JPEG) {
+            uint8_t* px = nullptr;
+            uint32_t nx = 0, ny = 0, ch = 0;
+            if (!o.image_path) return set_error(RTOW_E_INVALID, "JPEG image mode without image_path");
+            const int rc = rtow_image_load_jpeg(o.image_path, &px, &nx, &ny, &ch);
+            if (rc != RTOW_OK) return rc;
+            if (ch != 3) {
+                rtow_image_free(px);
+                return set_error(RTOW_E_UNSUPPORTED, "JPEG texture is not 3-channel (ImageTexture reads RGB)");
+            }
+            Image im;
+            im.nx = (int)nx;
+            im.ny = (int)ny;
+            im.rgb.assign(px, px + (size_t)nx * ny * 3);
+            rtow_image_free(px);
+            out.images.push_back(std::move(im));
+            earth = &out.images.back();
         } else if (o.image_mode == RTOW_IMAGE_RAW) {
             Image im;
             if (!o.image_path || o.image_nx == 0 || o.image_ny == 0 ||

@@ -22,8 +22,8 @@ SCENE_THREE_SPHERE, SCENE_RANDOM_NED, SCENE_CORNELL_NED, SCENE_CORNELL_SMOKE = 1
 SCENE_FINAL_NED = 5
 SCENES = {"three_sphere": SCENE_THREE_SPHERE, "random_ned": SCENE_RANDOM_NED, "cornell": SCENE_CORNELL_NED,
           "cornell_smoke": SCENE_CORNELL_SMOKE, "final_ned": SCENE_FINAL_NED}
-IMAGE_NONE, IMAGE_SYNTHETIC, IMAGE_RAW = 0, 1, 2
-IMAGES = {"none": IMAGE_NONE, "synthetic": IMAGE_SYNTHETIC, "raw": IMAGE_RAW}
+IMAGE_NONE, IMAGE_SYNTHETIC, IMAGE_RAW, IMAGE_JPEG = 0, 1, 2, 3
+IMAGES = {"none": IMAGE_NONE, "synthetic": IMAGE_SYNTHETIC, "raw": IMAGE_RAW, "jpeg": IMAGE_JPEG}
 FLAG_STATS = 1
 
 
@@ -116,6 +116,11 @@ def lib():
         "rtow_render_tiles_device": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, vp,
                                       ctypes.POINTER(Stats)], i32),
         "rtow_assemble_device": ([vp, u32, u32, u32, vp, u32, vp, vp], i32),
+        "rtow_image_decode_jpeg": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp), ctypes.POINTER(u32),
+                                    ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
+        "rtow_image_load_jpeg": ([ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                  ctypes.POINTER(u32)], i32),
+        "rtow_image_free": ([vp], None),
     }
     for name, (args, res) in sig.items():
         if not hasattr(L, name) and os.environ.get("RTOW_LIB"):
@@ -226,6 +231,22 @@ def tile_count(width, height):
 
 def rank_tile_count(width, height, rank, world):
     return lib().rtow_rank_tile_count(width, height, rank, world)
+
+
+def decode_jpeg(data):
+    """JPEG bytes -> (H, W, C) uint8 array, as the reference's stbi_load(.., 0) returns it."""
+    import numpy as np
+
+    L = lib()
+    px, nx, ny, ch = ctypes.c_void_p(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    check(L.rtow_image_decode_jpeg(bytes(data), len(data), ctypes.byref(px), ctypes.byref(nx), ctypes.byref(ny),
+                                   ctypes.byref(ch)), "rtow_image_decode_jpeg")
+    try:
+        n = nx.value * ny.value * ch.value
+        out = np.frombuffer(ctypes.string_at(px.value, n), dtype=np.uint8).reshape(ny.value, nx.value, ch.value)
+        return out.copy()
+    finally:
+        L.rtow_image_free(px)
 
 
 def synthetic_image(nx, ny):

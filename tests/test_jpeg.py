@@ -1,0 +1,71 @@
+"""The JPEG reader on the texture path (rtow_image_decode_jpeg,
+ray-tracing-one-weekend_amd/csrc/rtow_jpeg.cpp) returns the bytes the
+reference's own stb_image.h v2.22 returns (scenes.h:140: stbi_load(path, ..,
+0)) -- bit for bit.
+
+Fixtures: tests/golden/jpeg/make_jpeg_golden.py (PIL-encoded variants:
+sampling 4:2:0/4:2:2/4:4:4, grayscale, CMYK, progressive, restart markers,
+odd sizes; decoded by oracle/_ref/ref_harness `decode`, the reference's stb).
+Where /root/reference is present (build container) the reference's own
+input_images are decoded by both too.  CPU only: host code."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import rtow
+import scene_io as sio
+
+JDIR = os.path.join(sio.GOLDEN, "jpeg")
+MANIFEST = json.load(open(os.path.join(JDIR, "manifest.json")))
+REF_IMAGES = "/root/reference/rayTracingOneWeekend/input_images"
+HARNESS = os.path.join(sio.REPO, "oracle", "_ref", "ref_harness")
+
+
+def _img(path):
+    raw = open(path, "rb").read()
+    nx, ny, n = (int(v) for v in np.frombuffer(raw[:12], np.uint32))
+    return np.frombuffer(raw[12:], np.uint8).reshape(ny, nx, n)
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"]])
+def test_decode_matches_reference_stb(name):
+    got = rtow.decode_jpeg(open(os.path.join(JDIR, name + ".jpg"), "rb").read())
+    ref = _img(os.path.join(JDIR, name + ".img"))
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)
+
+
+def test_load_from_file_and_scene_build(tmp_path):
+    """RTOW_IMAGE_JPEG: the scene builder reads the texture through the same
+    decoder (random scene: the earth texture of scenes.h:140)."""
+    path = os.path.join(JDIR, "yuv420_q75.jpg")
+    ref = _img(os.path.join(JDIR, "yuv420_q75.img"))
+    s = rtow.Scene.build("random_ned", n=100, image="jpeg", image_path=path)
+    d = sio.scene_dict(s)
+    assert len(d["images"]) == 1 and int(d["images"][0]["nx"]) == ref.shape[1]
+    assert bytes(d["texels"][: ref.size]) == ref.tobytes()
+
+
+def test_corrupt_input_fails_loudly():
+    data = open(os.path.join(JDIR, "yuv420_q75.jpg"), "rb").read()
+    with pytest.raises(rtow.RtowError):
+        rtow.decode_jpeg(b"\x00" + data[1:])
+    with pytest.raises(rtow.RtowError):
+        rtow.decode_jpeg(data[:40])
+
+
+@pytest.mark.skipif(not (os.path.isdir(REF_IMAGES) and os.access(HARNESS, os.X_OK)),
+                    reason="needs /root/reference and oracle/_ref/ref_harness (build container)")
+def test_reference_input_images_bit_exact(tmp_path):
+    """Every image the reference ships (1_earth_8k.jpg is baseline 4:2:0,
+    earth1300x1300.jpg progressive) against the reference's stb."""
+    for f in sorted(os.listdir(REF_IMAGES)):
+        if not f.endswith(".jpg"):
+            continue
+        out = str(tmp_path / (f + ".img"))
+        subprocess.run([HARNESS, "decode", os.path.join(REF_IMAGES, f), out], check=True)
+        got = rtow.decode_jpeg(open(os.path.join(REF_IMAGES, f), "rb").read())
+        assert np.array_equal(got, _img(out)), f
