@@ -211,6 +211,8 @@ __device__ __forceinline__ F3 inv_dir(F3 d) { return f3(1.0f / d.x, 1.0f / d.y, 
 // Translate(..., (0,0,1000)): in the BVH frame o.z ~ -1000, boxes ~1 away) and
 // then culls subtrees holding the true closest hit.  x - o is exact for
 // nearby planes (Sterbenz), so the error stays within a few ulp of t.
+// (The simple-scene kernel uses the one-FMA form in the world frame:
+// SlabRayF below.)
 struct SlabRay {
     F3 o, inv;
 };
@@ -241,6 +243,41 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
     // differed from the oracle by > 1e-6; by 2^-13 or 2^-9, 2 (the same two
     // in both: transcendentals), at no measurable cost (tools/diverge.py).
     const float tf = fminf(ex * 1.001953125f, tmax_c);
+    tnear = tn;
+    return tn <= tf;
+}
+
+// The simple-scene kernel's slab test: each plane is x*(1/d) - o*(1/d), one
+// FMA with o*(1/d) hoisted per ray, in the world frame (the DNode boxes moved
+// there by shiftBoxes: the rays' origins lie near the boxes).  The error of a
+// plane's t is at most 2^-24 (|o/d| + |t|) (plus the world-frame origin's own
+// rounding, also below 2^-24 |o/d|), so the exit is widened by 2^-9 relative
+// (covering the |t| part) and by werr = 2^-21 max|o/d| absolute: culling
+// stays conservative in any frame.  1/d is clamped to +-2^64 (a zero
+// direction component gives planes at +-huge instead of +-inf, so x*(1/d) -
+// o*(1/d) never forms inf - inf; with |1/d| > 2^64 every plane of the axis
+// lies beyond any distance the scene has either way).
+struct SlabRayF {
+    F3 oi, inv;
+    float werr;
+};
+__device__ __forceinline__ SlabRayF slab_ray_f(F3 o, F3 d) {
+    constexpr float BIG = 0x1p64f;
+    SlabRayF s;
+    const F3 inv = inv_dir(d);
+    s.inv = f3(fminf(fmaxf(inv.x, -BIG), BIG), fminf(fmaxf(inv.y, -BIG), BIG), fminf(fmaxf(inv.z, -BIG), BIG));
+    s.oi = mulv(o, s.inv);
+    s.werr = fmaxf(fmaxf(fabsf(s.oi.x), fabsf(s.oi.y)), fabsf(s.oi.z)) * 0x1p-21f;
+    return s;
+}
+__device__ __forceinline__ bool slab_f(float x0, float x1, float y0, float y1, float z0, float z1, const SlabRayF& q,
+                                       float tmin, float tmax_c, float& tnear) {
+    const float tx0 = fmaf(x0, q.inv.x, -q.oi.x), tx1 = fmaf(x1, q.inv.x, -q.oi.x);
+    const float ty0 = fmaf(y0, q.inv.y, -q.oi.y), ty1 = fmaf(y1, q.inv.y, -q.oi.y);
+    const float tz0 = fmaf(z0, q.inv.z, -q.oi.z), tz1 = fmaf(z1, q.inv.z, -q.oi.z);
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    const float tf = fminf(fmaf(ex, 1.001953125f, q.werr), tmax_c);  // see slab()
     tnear = tn;
     return tn <= tf;
 }
@@ -585,7 +622,9 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
 template <int STACK, int BS, bool PROF>
 __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t root, const Ray& r, float tmin,
                                  float& bt, uint32_t* stk, uint32_t& overflow, Prof& prof) {
-    const SlabRay q = slab_ray(r);
+    // the boxes sit in the world frame (DevScene::tshift, see SlabRay): the
+    // ray's origin there, from its origin in the BVH's frame
+    const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
     const float a = dot(r.d, r.d);
     const float ra = 1.0f / a;
     const float time = r.time;
@@ -642,7 +681,7 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
+            hb = slab_f(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
         }
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
@@ -654,7 +693,7 @@ __device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
+            ha = slab_f(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
         }
         // one back-edge, one exit: push / descend / pop are predicated updates
         const uint32_t NONE = mkref(DK_NONE, 0);
@@ -1869,6 +1908,7 @@ struct HostLayout {
     std::vector<uint32_t> rect_anc;  // DevScene::rect_anc
     std::vector<float> abox;         // DevScene::abox
     std::vector<DProg> prog;         // DevScene::prog
+    float tshift[3] = {0.0f, 0.0f, 0.0f};  // DevScene::tshift
 };
 
 // ---------------------------------------------------------------------------
@@ -2486,6 +2526,39 @@ bool rebuildSah(HostLayout& L) {
     return true;
 }
 
+// A simple scene whose root chain is translations only: its DNode boxes move
+// to the world frame (rounded outward), where the rays' origins lie near them
+// and the one-FMA slab planes stay tight (SlabRay); the kernel shifts each
+// ray's origin by the same float offset.  Sphere slots stay in the BVH frame:
+// their tests are the reference's arithmetic.
+void shiftBoxes(HostLayout& L) {
+    float t[3] = {0.0f, 0.0f, 0.0f};
+    for (uint32_t k = 0; k < L.root_chain_n; k++) {
+        if ((L.root_chain[k] >> KIND_SHIFT) != DK_TRANSLATE) return;
+        const DInst& I = L.inst[L.root_chain[k] & INDEX_MASK];
+        for (int a = 0; a < 3; a++) t[a] += I.p[a];
+    }
+    if (t[0] == 0.0f && t[1] == 0.0f && t[2] == 0.0f) return;
+    auto down = [](double v) {
+        float f = (float)v;
+        return (double)f > v ? std::nextafter(f, -INFINITY) : f;
+    };
+    auto up = [](double v) {
+        float f = (float)v;
+        return (double)f < v ? std::nextafter(f, INFINITY) : f;
+    };
+    for (DNode& d : L.node)
+        for (int k = 0; k < 2; k++) {
+            float* f = k == 0 ? d.a : d.b;
+            if (((k == 0 ? d.ref_a : d.ref_b) >> KIND_SHIFT) != DK_BVH) continue;
+            for (int a = 0; a < 3; a++) {
+                f[a] = down((double)f[a] + t[a]);
+                f[3 + a] = up((double)f[3 + a] + t[a]);
+            }
+        }
+    for (int a = 0; a < 3; a++) L.tshift[a] = t[a];
+}
+
 // true when everything below `ref` is BvhNodes and spheres
 bool onlyBvhSpheres(const HostLayout& L, uint32_t ref, int depth = 0) {
     const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
@@ -3066,6 +3139,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
                 }
             }
             if (tree == RTOW_TREE_SAH && (L.bvh_root >> KIND_SHIFT) == DK_BVH) rebuildSah(L);
+            shiftBoxes(L);
         }
     }
     for (uint32_t i = 0; i < s.n_materials; i++) {
@@ -3627,6 +3701,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.rect_anc = (const uint32_t*)(b + o_anc);
     d.abox = (const float*)(b + o_abox);
     d.prog = (const DProg*)(b + o_prog);
+    for (int a = 0; a < 3; a++) d.tshift[a] = L.tshift[a];
     d.root = L.root;
     d.stack_need = L.stack_need;
     d.has_media = L.has_media ? 1u : 0u;

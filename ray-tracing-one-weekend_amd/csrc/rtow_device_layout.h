@@ -225,6 +225,7 @@ struct DevScene {
     uint32_t root_chain[4];
     uint32_t bvh_root;       // root below the chain
     uint32_t n_node;         // DNode count (simple scenes)
+    float tshift[3];         // simple scenes: world-frame offset of the DNode boxes (shiftBoxes)
     uint32_t gnode;          // general scene: node[i] is the DNode twin of bvh[i] (DK_BVH steps read it)
 };
 
