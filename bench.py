@@ -208,6 +208,21 @@ def cpu_baseline(scene, cam, args, threads):
     return base, bytes_per_ray, counts
 
 
+def frame_step(render, assemble, slab, gathered, rank, world, dist=None):
+    """One bench step: this rank renders its 8x8-tile slab (`render(slab)`),
+    one gather brings every rank's slab to rank 0 (torch.distributed: RCCL
+    over xGMI on the GPUs, gloo in tests/test_distributed.py), rank 0
+    assembles the frame (`assemble(gathered)`).  Returns render's stats."""
+    st = render(slab)
+    if world > 1:
+        dist.gather(slab, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+    else:
+        gathered[0].copy_(slab)
+    if rank == 0:
+        assemble(gathered)
+    return st
+
+
 def main():
     args = parse()
     import torch
@@ -242,14 +257,9 @@ def main():
     p = rtow.params(W, H, spp, seed=args.seed, rank=rank, world=world)
 
     def step():
-        st = ctx.render_tiles_device(cam, p, slab.data_ptr(), None, stream)
-        if distributed:
-            dist.gather(slab, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-        else:
-            gathered[0].copy_(slab)
-        if rank == 0:
-            ctx.assemble_device(W, H, world, gathered.data_ptr(), stride, frame.data_ptr(), stream)
-        return st
+        return frame_step(lambda sl: ctx.render_tiles_device(cam, p, sl.data_ptr(), None, stream),
+                          lambda g: ctx.assemble_device(W, H, world, g.data_ptr(), stride, frame.data_ptr(), stream),
+                          slab, gathered, rank, world, dist)
 
     for _ in range(args.warmup):
         step()

@@ -1,7 +1,8 @@
-"""Multi-rank path on CPU (gloo, world size 2): every rank renders its tile
-slab (with the C oracle standing in for the GPU kernel -- the partition,
-gather and assembly are what is under test), one gather to rank 0, rank 0
-assembles the frame; it must equal the single-rank frame bit for bit."""
+"""Multi-rank path on CPU (gloo, world size 2), driven through bench.py's own
+step (bench.frame_step: render the rank's slab, one gather to rank 0, rank 0
+assembles): the C oracle stands in for the GPU kernel and rtow.assemble for
+assemble_kernel -- the partition, the gather and the assembly are what is
+under test.  The frame must equal the single-rank frame bit for bit."""
 import os
 import socket
 
@@ -39,15 +40,25 @@ def _worker(rank, world, port, W, H, spp, out_path):
     p = sio.default_params(W, H, spp, seed=3)
     idx = rtow.rank_pixels(W, H, rank, world)
     stride = rtow.rank_tile_count(W, H, 0, world) * 64
-    slab = torch.zeros((stride, 3), dtype=torch.float32)
+    sys.path.insert(0, os.path.dirname(here))
+    import bench
+
+    # bench.py's buffers: a BGRA8 slab per rank, [world, slab] on rank 0
+    slab = torch.zeros(stride * 4, dtype=torch.uint8)
+    gathered = torch.zeros((world, stride * 4), dtype=torch.uint8) if rank == 0 else None
     valid = idx >= 0
-    lin, _, _ = sio.oracle_render(scene.view_ptr, cam, p, pixels=idx[valid].astype(np.uint32), threads=2)
-    slab[: idx.size][torch.from_numpy(valid)] = torch.from_numpy(lin)
-    gathered = [torch.zeros_like(slab) for _ in range(world)] if rank == 0 else None
-    dist.gather(slab, gathered, dst=0)
-    if rank == 0:
-        frame = rtow.assemble(torch.stack(gathered).numpy(), W, H, world)
-        np.save(out_path, frame)
+
+    def render(sl):  # the oracle in place of rtow_render_tiles_device
+        _, bgra, cnt = sio.oracle_render(scene.view_ptr, cam, p, pixels=idx[valid].astype(np.uint32), threads=2)
+        view = sl.view(stride, 4)
+        view[: idx.size][torch.from_numpy(valid)] = torch.from_numpy(bgra.reshape(-1, 4))
+        return cnt
+
+    def assemble(g):  # rtow.assemble: the numpy mirror of assemble_kernel
+        np.save(out_path, rtow.assemble(g.view(world, stride, 4).numpy(), W, H, world))
+
+    cnt = bench.frame_step(render, assemble, slab, gathered, rank, world, dist)
+    assert cnt.samples == int(valid.sum()) * spp
     dist.barrier()
     dist.destroy_process_group()
 
@@ -60,8 +71,8 @@ def test_gloo_world2_gather_assembles_single_rank_frame(W, H, tmp_path):
     frame = np.load(out)
     scene = rtow.Scene.build("cornell_smoke")
     cam = sio.RtowCamera.from_buffer_copy(bytes(rtow.camera_main(W, H)))
-    full, _, _ = sio.oracle_render(scene.view_ptr, cam, sio.default_params(W, H, spp, seed=3))
-    assert np.array_equal(frame.reshape(-1, 3), full)
+    _, full, _ = sio.oracle_render(scene.view_ptr, cam, sio.default_params(W, H, spp, seed=3))
+    assert np.array_equal(frame.reshape(-1, 4), full.reshape(-1, 4))
 
 
 @pytest.mark.parametrize("W,H,world", [(37, 23, 3), (8, 8, 4), (1920, 1080, 8)])
