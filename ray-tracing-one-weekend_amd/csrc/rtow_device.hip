@@ -1652,6 +1652,11 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 t_mark = t_now;
             }
             if (hit) finalize<true>(S, prim, bt, ray, rec);
+            if constexpr (PROF) {
+                const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                prof.cyc_fin += t_now - t_mark;
+                t_mark = t_now;
+            }
         } else {
             // park the path state the traversal does not need (COLD)
             cold[0 * BS] = __float_as_uint(acc.x);
@@ -1734,7 +1739,17 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         bool done;
         F3 contrib;
         const F3 tv = texture_at<BS>(S, T, P, hit, rec, depth, stk - lane);
+        if constexpr (PROF && SIMPLE) {  // simple scenes: texture / shading split of the wave cycles
+            const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+            prof.cyc_item[0] += t_now - t_mark;
+            t_mark = t_now;
+        }
         shade_segment(S, P, hit, rec, tv, ray, thr, depth, rng, contrib, done);
+        if constexpr (PROF && SIMPLE) {
+            const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+            prof.cyc_item[1] += t_now - t_mark;
+            t_mark = t_now;
+        }
         if (done) {
             acc = add(acc, contrib);
             s++;
@@ -1770,14 +1785,12 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         if (lane == 0) {  // s_memtime is per wave: lane 0's copy is the wave's
             atomicAdd(&counters[7], prof.cyc_trav);
             atomicAdd(&counters[8], prof.cyc_other);
-            if constexpr (!SIMPLE) {
-                for (int k = 0; k < 8; k++) {
-                    atomicAdd(&counters[16 + k], prof.cyc_item[k]);
-                    atomicAdd(&counters[24 + k], prof.visits_item[k]);
-                }
-                atomicAdd(&counters[32], prof.cyc_fin);
-                atomicAdd(&counters[33], prof.cyc_chain);
+            for (int k = 0; k < 8; k++) {
+                atomicAdd(&counters[16 + k], prof.cyc_item[k]);
+                atomicAdd(&counters[24 + k], prof.visits_item[k]);
             }
+            atomicAdd(&counters[32], prof.cyc_fin);
+            atomicAdd(&counters[33], prof.cyc_chain);
         }
     }
 }
@@ -3519,7 +3532,13 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
         std::fprintf(stderr, "rtow-profile: wave cycles traversal %.3g other %.3g (traversal share %.3f)\n",
                      (double)host_ctr[7], (double)host_ctr[8],
                      (double)host_ctr[7] / (double)(host_ctr[7] + host_ctr[8] + host_ctr[32]));
-    if (c->profile && host_ctr[32]) {
+    if (c->profile && host_ctr[32] && c->scene.simple) {
+        const double tot = (double)(host_ctr[7] + host_ctr[8] + host_ctr[32] + host_ctr[16] + host_ctr[17]);
+        std::fprintf(stderr, "rtow-profile: simple: wave cycles traversal %.3f finalize %.3f texture %.3f shade %.3f "
+                             "refill+camera+sums %.3f\n",
+                     host_ctr[7] / tot, host_ctr[32] / tot, host_ctr[16] / tot, host_ctr[17] / tot, host_ctr[8] / tot);
+    }
+    if (c->profile && host_ctr[32] && !c->scene.simple) {
         const double tot = (double)(host_ctr[7] + host_ctr[8] + host_ctr[32]);
         std::fprintf(stderr, "rtow-profile: general traversal iterations lane %llu wave %llu (SIMD eff %.3f, %.2f per "
                              "ray, node steps %.2f per ray)\n",

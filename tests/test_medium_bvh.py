@@ -55,12 +55,17 @@ def test_oracle_medium_bvh_matches_reference_bit_exact():
 
 
 @pytest.mark.gpu
-def test_gpu_medium_bvh_matches_reference(gpu_ctx):
+@pytest.mark.parametrize("tree", ["sah", "reference"])
+def test_gpu_medium_bvh_matches_reference(gpu_ctx, tree):
     c = CASE
     W, H = c["width"], c["height"]
     d, arrays, ocam, op = _setup()
-    gpu_ctx.upload(sio.ArrayScene(d))
-    bgra, lin, st = gpu_ctx.render(rtow.camera_main(W, H), rtow.params(W, H, c["spp"], seed=c["seed"]))
+    gpu_ctx.set_tree(tree)
+    try:
+        gpu_ctx.upload(sio.ArrayScene(d))
+        bgra, lin, st = gpu_ctx.render(rtow.camera_main(W, H), rtow.params(W, H, c["spp"], seed=c["seed"]))
+    finally:
+        gpu_ctx.set_tree("sah")
     glin, gbgra = sio.golden_image("medium_bvh", W, H)
     a = np.asarray(lin, np.float64).reshape(-1, 3)
     rms = np.sqrt(np.mean((a - glin.reshape(-1, 3)) ** 2, axis=0))
