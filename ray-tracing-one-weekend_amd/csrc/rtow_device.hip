@@ -415,6 +415,23 @@ __device__ __forceinline__ bool rect_t(const DRect& q, const Ray& r, const F3& i
     return true;
 }
 
+// rect_t with the axes known at compile time: K the plane's axis, I and J the
+// in-plane ones (rect_axes: XY K=2 I=0 J=1, XZ K=1 I=0 J=2, YZ K=0 I=1 J=2);
+// the same float operations, without selecting components at run time
+template <int A>
+__device__ __forceinline__ float cmp3(const F3& v) { return A == 0 ? v.x : (A == 1 ? v.y : v.z); }
+template <int K, int I, int J>
+__device__ __forceinline__ bool rect_t_ax(float a0, float a1, float b0, float b1, float k, const Ray& r, const F3& inv,
+                                          float t0, float t1, float& t) {
+    const float tt = div_by_any(k - cmp3<K>(r.o), cmp3<K>(r.d), cmp3<K>(inv));
+    if (tt < t0 || tt > t1) return false;
+    const float x = cmp3<I>(r.o) + tt * cmp3<I>(r.d);
+    const float y = cmp3<J>(r.o) + tt * cmp3<J>(r.d);
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t = tt;
+    return true;
+}
+
 // AABB::hit (aabb.h:22-43) exactly: true divisions, ffmin/ffmax, `tmax <= tmin`
 // (a NaN comparison does not reject).  b: min xyz, 0, max xyz, 0.
 __device__ __forceinline__ bool ref_slab(float mn, float mx, float o, float d, float& tmin, float& tmax) {
@@ -478,6 +495,55 @@ __device__ __forceinline__ bool ref_skips_hit(const DevScene& S, uint32_t rect, 
     const float ex = (fabsf(q.a0) + fabsf(q.a1) + 1.0f) * 0x1p-14f, ey = (fabsf(q.b0) + fabsf(q.b1) + 1.0f) * 0x1p-14f;
     const bool edge = x - q.a0 < ex || q.a1 - x < ex || y - q.b0 < ey || q.b1 - y < ey;
     return edge && !ref_reaches_rect(S, rect, r, tmin);
+}
+
+// A Box's six sides (DBox6) in their list order (box.h:29-38), each tested as
+// the rectangle-list loop tests it: the interval [tmin, bt] shrinks as sides
+// are taken, exact ties go by the tie keys, and in strict mode a side counts
+// only where the reference's boxes reach it.  Returns whether a side was taken.
+__device__ __forceinline__ bool wins_tie(const DevScene& S, uint32_t cand, uint32_t best);
+template <int K, int I, int J>
+__device__ __forceinline__ void box6_side(const DevScene& S, float a0, float a1, float b0, float b1, float k,
+                                          uint32_t rect, const Ray& r, const F3& inv, float tmin, float& bt,
+                                          uint32_t& best, bool strict, bool& found) {
+    float t;
+    const uint32_t ref = mkref(DK_RECT, rect);
+    if (rect_t_ax<K, I, J>(a0, a1, b0, b1, k, r, inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, best)) &&
+        (!strict || ref_reaches_rect(S, rect, r, tmin))) {
+        bt = t;
+        best = ref;
+        found = true;
+    }
+}
+__device__ __forceinline__ bool box6_scan(const DevScene& S, uint32_t bi, const Ray& r, const F3& inv, float tmin,
+                                          float& bt, uint32_t& best, bool strict) {
+    const float4 lo = reinterpret_cast<const float4*>(S.box6 + bi)[0];
+    const float4 hi = reinterpret_cast<const float4*>(S.box6 + bi)[1];
+    const uint32_t f = __float_as_uint(lo.w);
+    bool found = false;
+    box6_side<2, 0, 1>(S, lo.x, hi.x, lo.y, hi.y, hi.z, f + 0, r, inv, tmin, bt, best, strict, found);  // XY at z1 (flipped)
+    box6_side<2, 0, 1>(S, lo.x, hi.x, lo.y, hi.y, lo.z, f + 1, r, inv, tmin, bt, best, strict, found);  // XY at z0
+    box6_side<1, 0, 2>(S, lo.x, hi.x, lo.z, hi.z, hi.y, f + 2, r, inv, tmin, bt, best, strict, found);  // XZ at y1
+    box6_side<1, 0, 2>(S, lo.x, hi.x, lo.z, hi.z, lo.y, f + 3, r, inv, tmin, bt, best, strict, found);  // XZ at y0 (flipped)
+    box6_side<0, 1, 2>(S, lo.y, hi.y, lo.z, hi.z, hi.x, f + 4, r, inv, tmin, bt, best, strict, found);  // YZ at x1
+    box6_side<0, 1, 2>(S, lo.y, hi.y, lo.z, hi.z, lo.x, f + 5, r, inv, tmin, bt, best, strict, found);  // YZ at x0 (flipped)
+    return found;
+}
+// ConstantMedium's boundary query over a Box (MB_BOX6): the nearest side hit
+// in [lo_t, near] (which side does not matter), near shrinking as sides hit
+__device__ __forceinline__ bool box6_nearest(const DevScene& S, uint32_t bi, const Ray& r, const F3& inv, float lo_t,
+                                             float& near) {
+    const float4 lo = reinterpret_cast<const float4*>(S.box6 + bi)[0];
+    const float4 hi = reinterpret_cast<const float4*>(S.box6 + bi)[1];
+    bool f = false;
+    float t;
+    if (rect_t_ax<2, 0, 1>(lo.x, hi.x, lo.y, hi.y, hi.z, r, inv, lo_t, near, t)) near = t, f = true;
+    if (rect_t_ax<2, 0, 1>(lo.x, hi.x, lo.y, hi.y, lo.z, r, inv, lo_t, near, t)) near = t, f = true;
+    if (rect_t_ax<1, 0, 2>(lo.x, hi.x, lo.z, hi.z, hi.y, r, inv, lo_t, near, t)) near = t, f = true;
+    if (rect_t_ax<1, 0, 2>(lo.x, hi.x, lo.z, hi.z, lo.y, r, inv, lo_t, near, t)) near = t, f = true;
+    if (rect_t_ax<0, 1, 2>(lo.y, hi.y, lo.z, hi.z, hi.x, r, inv, lo_t, near, t)) near = t, f = true;
+    if (rect_t_ax<0, 1, 2>(lo.y, hi.y, lo.z, hi.z, lo.x, r, inv, lo_t, near, t)) near = t, f = true;
+    return f;
 }
 
 // Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
@@ -620,7 +686,7 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
 // next node fetch at once while the LDS read of the new top is in flight.
 // Returns the winning sphere ref or DK_NONE.
 template <int STACK, int BS, bool PROF>
-__device__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t root, const Ray& r, float tmin,
+__device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t root, const Ray& r, float tmin,
                                  float& bt, uint32_t* stk, uint32_t& overflow, Prof& prof) {
     // the boxes sit in the world frame (DevScene::tshift, see SlabRay): the
     // ray's origin there, from its origin in the BVH's frame
@@ -777,6 +843,19 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
     if (M.bkind == MB_SPHERE) {
         const Sph s = load_sph(S.sph + (M.boundary & INDEX_MASK));
         two = S.unit_time ? sphere_boundary<true>(s, r, a, t1, t2) : sphere_boundary<false>(s, r, a, t1, t2);
+    } else if (M.bkind == MB_BOX6) {
+        // the same two queries over a Box's sides (box6_nearest)
+        const Ray rb = chain_ray(S, M.bchain, wray);
+        const F3 inv = inv_dir(rb.d);
+        float near = FLT_MAX;
+        if (box6_nearest(S, M.bfirst, rb, inv, -FLT_MAX, near)) {
+            t1 = near;
+            near = FLT_MAX;
+            if (box6_nearest(S, M.bfirst, rb, inv, (float)((double)t1 + 0.0001), near)) {
+                t2 = near;
+                two = true;
+            }
+        }
     } else if (M.bkind == MB_RECTS) {
         // boundary->hit(-FLT_MAX, FLT_MAX) then boundary->hit(t1 + 0.0001,
         // FLT_MAX) over instances of a Box: the nearest rectangle hit in each
@@ -897,6 +976,9 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
         } else if (kind == DK_RECTS) {
             // a list of rectangles: scanned in order, closed interval, as hitableList.h
             const DList R = S.list[idx];
+            if (R.box6) {  // a Box's sides: the unrolled scan
+                if (box6_scan(S, R.box6 - 1, r, q.inv, tmin, bt, best.prim, strict)) found = true;
+            } else
             for (uint32_t j = 0; j < R.count; j++) {
                 const uint32_t ref = mkref(DK_RECT, R.first + j);
                 float t;
@@ -1062,7 +1144,9 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             __builtin_amdgcn_s_waitcnt(0);
             prof->cyc_chain += __builtin_amdgcn_s_memtime() - tc;
         }
-        if (T.kind == TOP_RECTS) {
+        if (T.kind == TOP_BOX6) {
+            if (box6_scan(S, T.a, r, inv, tmin, bt, bp, strict)) found = true;
+        } else if (T.kind == TOP_RECTS) {
             for (uint32_t k = 0; k < T.b; k++) {
                 const uint32_t ref = mkref(DK_RECT, T.a + k);
                 float t;
@@ -1121,7 +1205,7 @@ __device__ __forceinline__ void sphere_uv(F3 p, float& u, float& v) {
 // instance chain), the leaf's record, then the instances' way out.
 // SIMPLE: every leaf sits under the root chain (kernel-argument registers).
 template <bool SIMPLE>
-__device__ void finalize(const DevScene& S, uint32_t prim, float t, const Ray& wray, Rec& rec) {
+__device__ __forceinline__ void finalize(const DevScene& S, uint32_t prim, float t, const Ray& wray, Rec& rec) {
     const uint32_t kind = prim >> KIND_SHIFT;
     const uint32_t idx = prim & INDEX_MASK;
     const uint32_t chain =
@@ -1170,7 +1254,7 @@ struct Tables {
     const uint32_t* perm;
 };
 
-__device__ float perlin_noise(const Tables& T, F3 p) {
+__device__ __forceinline__ float perlin_noise(const Tables& T, F3 p) {
     const float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
     const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
     const int i = (int)fx, j = (int)fy, k = (int)fz;
@@ -1260,7 +1344,7 @@ __device__ __forceinline__ uint32_t resolve_tex(const DevScene& S, uint32_t ti, 
 
 // Texture::value of a resolved (non-checker) texture; `turb` is
 // Perlin::turbulance(p) when it is a NoiseTexture (wave_turbulence)
-__device__ F3 leaf_tex_value(const DevScene& S, uint32_t ti, float u, float v, F3 p, float turb) {
+__device__ __forceinline__ F3 leaf_tex_value(const DevScene& S, uint32_t ti, float u, float v, F3 p, float turb) {
     const DTex t = S.tex[ti];
     if (t.kind == RTOW_TEX_CONSTANT) return f3(t.f[0], t.f[1], t.f[2]);
     if (t.kind == RTOW_TEX_NOISE) {  // texture.h:44-48
@@ -1329,7 +1413,7 @@ __device__ __forceinline__ float schlick(float cosine, float ri) {
 // Lambertian, Metal and Isotropic each start with randomInUnitSphere() and
 // draw nothing else, so one rejection loop serves all three (lanes of a wave
 // with different materials loop together, not one material after another).
-__device__ bool scatter(const DMat& m, const Ray& in, const Rec& rec, F3 tv, Rng& g, F3& atten, Ray& out) {
+__device__ __forceinline__ bool scatter(const DMat& m, const Ray& in, const Rec& rec, F3 tv, Rng& g, F3& atten, Ray& out) {
     F3 rius = f3(0, 0, 0);
     if (m.kind == RTOW_MAT_LAMBERTIAN || m.kind == RTOW_MAT_METAL || m.kind == RTOW_MAT_ISOTROPIC)
         rius = random_in_unit_sphere(g);
@@ -1921,6 +2005,7 @@ struct HostLayout {
     std::vector<uint32_t> rect_anc;  // DevScene::rect_anc
     std::vector<float> abox;         // DevScene::abox
     std::vector<DProg> prog;         // DevScene::prog
+    std::vector<DBox6> box6;         // DevScene::box6
     float tshift[3] = {0.0f, 0.0f, 0.0f};  // DevScene::tshift
 };
 
@@ -2581,6 +2666,36 @@ bool onlyBvhSpheres(const HostLayout& L, uint32_t ref, int depth = 0) {
     return onlyBvhSpheres(L, L.bvh[idx].left, depth + 1) && onlyBvhSpheres(L, L.bvh[idx].right, depth + 1);
 }
 
+// A rectangle list that is a Box's six sides (box.h:29-38: XY at z1 and z0,
+// XZ at y1 and y0, YZ at x1 and x0, each spanning the box): its DBox6, whose
+// unrolled scan (box6_scan) performs the same tests in the same order.
+// Returns 1 + the DBox6 index, or 0.
+uint32_t detectBox6(HostLayout& L, uint32_t first, uint32_t count) {
+    if (count != 6) return 0;
+    const DRect* q = &L.rect[first];
+    const float x0 = q[0].a0, x1 = q[0].a1, y0 = q[0].b0, y1 = q[0].b1, z1 = q[0].k, z0 = q[1].k;
+    const float y1b = q[2].k, y0b = q[3].k, x1b = q[4].k, x0b = q[5].k;
+    auto same = [](float a, float b) { return std::memcmp(&a, &b, sizeof a) == 0; };
+    const uint32_t ax[6] = {0, 0, 1, 1, 2, 2};
+    for (int j = 0; j < 6; j++)
+        if ((q[j].axis & 3u) != ax[j]) return 0;
+    // XY sides: x, y bounds; XZ sides: x, z bounds; YZ sides: y, z bounds
+    const float zlo = q[2].b0, zhi = q[2].b1;
+    const bool ok = same(q[1].a0, x0) && same(q[1].a1, x1) && same(q[1].b0, y0) && same(q[1].b1, y1) &&
+                    same(q[2].a0, x0) && same(q[2].a1, x1) && same(q[3].a0, x0) && same(q[3].a1, x1) &&
+                    same(q[3].b0, zlo) && same(q[3].b1, zhi) && same(zlo, z0) && same(zhi, z1) &&
+                    same(q[4].a0, y0) && same(q[4].a1, y1) && same(q[4].b0, z0) && same(q[4].b1, z1) &&
+                    same(q[5].a0, y0) && same(q[5].a1, y1) && same(q[5].b0, z0) && same(q[5].b1, z1) &&
+                    same(y1b, y1) && same(y0b, y0) && same(x1b, x1) && same(x0b, x0);
+    if (!ok) return 0;
+    DBox6 b{};
+    b.lo[0] = x0, b.lo[1] = y0, b.lo[2] = z0;
+    b.hi[0] = x1, b.hi[1] = y1, b.hi[2] = z1;
+    b.first = first;
+    L.box6.push_back(b);
+    return (uint32_t)L.box6.size();
+}
+
 struct Converter {
     const rtow_scene& s;
     HostLayout& L;
@@ -2717,6 +2832,7 @@ struct Converter {
                 const uint32_t r0 = (uint32_t)L.rect.size();
                 for (uint32_t i = 0; i < h.b; i++) L.rect.push_back(L.rect[L.refs[first + i] & INDEX_MASK]);
                 L.list[slot] = DList{r0, h.b, 0, 0};
+                L.list[slot].box6 = detectBox6(L, r0, h.b);
                 ref = mkref(DK_RECTS, slot);
             }
             break;
@@ -3028,6 +3144,7 @@ void buildTop(HostLayout& L) {
             bool one = r.count > 0;
             for (uint32_t q = 1; q < r.count; q++) one = one && L.rect[r.first + q].chain == L.rect[r.first].chain;
             if (one) t = DTop{TOP_RECTS, r.first, r.count, L.rect[r.first].chain};
+            if (one && r.box6) t = DTop{TOP_BOX6, r.box6 - 1, r.count, L.rect[r.first].chain};
         } else if (k == DK_SPHERE) {
             t = DTop{TOP_SPHERE, i, 0, L.sph[i].chain};
         } else if (k == DK_MEDIUM && L.med[i].bkind != MB_ANY) {
@@ -3245,8 +3362,8 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
                 bool one = r.count > 0;
                 for (uint32_t q = 1; q < r.count; q++) one = one && L.rect[r.first + q].chain == L.rect[r.first].chain;
                 if (one) {
-                    M.bkind = MB_RECTS;
-                    M.bfirst = r.first;
+                    M.bkind = r.box6 ? MB_BOX6 : MB_RECTS;
+                    M.bfirst = r.box6 ? r.box6 - 1 : r.first;
                     M.bcount = r.count;
                     M.bchain = L.rect[r.first].chain;
                 }
@@ -3686,6 +3803,8 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_anc = pushBlob(blob, L.rect_anc), o_abox = pushBlob(blob, L.abox);
     if (L.prog.empty()) L.prog.push_back(DProg{});
     size_t o_prog = pushBlob(blob, L.prog);
+    if (L.box6.empty()) L.box6.push_back(DBox6{});
+    size_t o_box6 = pushBlob(blob, L.box6);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -3720,6 +3839,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.rect_anc = (const uint32_t*)(b + o_anc);
     d.abox = (const float*)(b + o_abox);
     d.prog = (const DProg*)(b + o_prog);
+    d.box6 = (const DBox6*)(b + o_box6);
     for (int a = 0; a < 3; a++) d.tshift[a] = L.tshift[a];
     d.root = L.root;
     d.stack_need = L.stack_need;

@@ -109,14 +109,27 @@ struct alignas(16) DChain {  // 32 B: instance refs, outermost first
 };
 
 struct alignas(16) DList {  // 16 B: children at refs[first .. first+count)
-    uint32_t first, count, pad0, pad1;
+    uint32_t first, count;
+    uint32_t box6;  // DK_RECTS: 1 + index in DevScene::box6 when the six rectangles are a Box's (0: no)
+    uint32_t pad1;
+};
+
+// A Box's six sides (box.h:25-41: XY at z1 and z0, XZ at y1 and y0, YZ at x1
+// and x0, in that list order) as its two corners: the six rectangle tests of
+// rect[first .. first+5] unrolled with their axes known at compile time
+// (box6_scan), same arithmetic, same order.
+struct alignas(16) DBox6 {  // 32 B
+    float lo[3];
+    uint32_t first;
+    float hi[3];
+    uint32_t pad;
 };
 
 // bkind: how the kernel queries the boundary (rtow_device.hip medium_hit):
 // MB_SPHERE a plain sphere (both roots from one quadratic), MB_RECTS instances
 // over a Box's rectangles rect[bfirst, +bcount) whose frame is chain bchain,
 // MB_ANY the general traversal.
-enum : uint32_t { MB_ANY = 0, MB_SPHERE = 1, MB_RECTS = 2 };
+enum : uint32_t { MB_ANY = 0, MB_SPHERE = 1, MB_RECTS = 2, MB_BOX6 = 3 };  // MB_BOX6: bfirst = box6 index
 struct alignas(16) DMedium {  // 32 B, constantMedium.h:21-23
     uint32_t boundary, phase_mat;
     float density;
@@ -155,7 +168,7 @@ struct alignas(16) DProg {  // 32 B; lo/hi read as ref_aabb_hit's (min xyz, -, m
 // Box's rectangles (MB_SPHERE / MB_RECTS) is asked right there (TOP_MEDIUM,
 // with the closest hit so far as its tmax, hitableList.h:30); anything else
 // goes to the general traversal.
-enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2, TOP_MEDIUM = 3 };
+enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2, TOP_MEDIUM = 3, TOP_BOX6 = 4 };  // BOX6: a = box6 index
 struct alignas(16) DTop {  // 16 B
     uint32_t kind;
     uint32_t a;      // GENERIC: item ref; RECTS: first rectangle; SPHERE: sphere; MEDIUM: medium
@@ -193,6 +206,7 @@ struct DevScene {
     const DChain* chains;
     const DTop* top;         // general scenes: the top-level list, n_top items (0: none)
     const DProg* prog;       // programs of the BvhNode subtrees that hold media (DK_PROG)
+    const DBox6* box6;       // Boxes among the rectangle lists (DList::box6, TOP_BOX6, MB_BOX6)
     uint32_t n_top;
     // Per rectangle: (offset << 8) | count of the boxes (8 floats each in
     // abox: min xyz, 0, max xyz, 0) of the reference BvhNodes above it in its

@@ -24,7 +24,7 @@ LIB = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "librtow_hip.so")
 
 # scratch bytes per lane allowed for the default (4-wave) general kernels,
 # by MODE (see DESIGN.md "Kernels"); the simple-scene kernels get none
-SCRATCH_BOUND = {0: 0, 2: 0, 4: 48, 3: 160, 5: 24}
+SCRATCH_BOUND = {0: 0, 2: 0, 4: 64, 3: 160, 5: 24}
 
 
 @pytest.fixture(scope="module")

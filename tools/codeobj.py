@@ -5,7 +5,8 @@ unit (magic "__CLANG_OFFLOAD_BUNDLE__", then entry count and per entry:
 offset, size, triple).  For every kernel of every gfx950 code object this
 returns what the code-object metadata records (VGPRs, SGPRs, scratch bytes
 per lane, spill counts, dynamic stack, LDS) and whether the kernel's code
-contains a call (s_swappc_b64 / s_setpc_b64): the shipped binary itself, not
+contains a call (s_swappc_b64, or an s_setpc_b64 that is not a long branch
+within the kernel): the shipped binary itself, not
 a recompilation.  Used by tests/test_build_resources.py.
 
   python tools/codeobj.py [path/to/librtow_hip.so]
@@ -88,13 +89,22 @@ def kernels(path):
         finally:
             os.unlink(co)
         calls, cur = {}, None
-        for line in dis.splitlines():
+        lines = dis.splitlines()
+        for i, line in enumerate(lines):
             m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
             if m:
                 cur = m.group(1)
                 calls.setdefault(cur, 0)
-            elif cur and re.search(r"\bs_(swappc|setpc)_b64\b", line):
+            elif cur and re.search(r"\bs_swappc_b64\b", line):
                 calls[cur] += 1
+            elif cur and re.search(r"\bs_setpc_b64\b", line):
+                # a long branch inside a huge kernel is s_getpc_b64 s[a:b];
+                # s_add_u32 sa, sa, off; s_addc_u32 sb, sb, 0; s_setpc_b64 s[a:b]
+                # (same function, target computed from its own pc): not a call
+                reg = re.search(r"s_setpc_b64\s+(s\[\d+:\d+\])", line)
+                prev = " ".join(lines[max(0, i - 4):i])
+                if not (reg and re.search(r"s_getpc_b64\s+" + re.escape(reg.group(1)), prev)):
+                    calls[cur] += 1
         for name, m in meta.items():
             res.append({"name": name, "vgpr": int(m.get("vgpr_count", -1)), "sgpr": int(m.get("sgpr_count", -1)),
                         "scratch": int(m.get("private_segment_fixed_size", -1)),
