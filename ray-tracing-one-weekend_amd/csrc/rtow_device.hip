@@ -1007,16 +1007,26 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                 continue;
             }
         } else if (kind == DK_TRANSLATE || kind == DK_ROTY || kind == DK_FLIP) {
-            // enter: the EXIT marker remembers the chain to restore
+            // enter: the EXIT marker remembers the chain to restore.  An
+            // instance's only child may be another instance (Translate(RotateY
+            // (...))): the whole run of them is entered at once -- the same
+            // transforms in the same order -- with one EXIT and the per-ray
+            // constants of the innermost frame only
             const DInst& I = S.inst[idx];
             if (sp < STACK) {
                 stk[sp * BLOCK] = mkref(DK_EXIT, I.parent_chain);
                 sp++;
                 r = apply_inst(S, cur, r);
+                cur = I.child;
+                for (int guard = 0; guard < MAXCHAIN; guard++) {
+                    const uint32_t ck = cur >> KIND_SHIFT;
+                    if (ck != DK_TRANSLATE && ck != DK_ROTY && ck != DK_FLIP) break;
+                    r = apply_inst(S, cur, r);
+                    cur = S.inst[cur & INDEX_MASK].child;
+                }
                 q = slab_ray(r);
                 a = dot(r.d, r.d);
                 ra = 1.0f / a;
-                cur = I.child;
                 continue;
             }
             overflow = 1;
