@@ -33,7 +33,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -576,7 +575,7 @@ __device__ __forceinline__ bool first_active_lane() {
 // exact tie the right one wins, as bvhNode.h:74-77 decides); of the inner
 // children that are hit the nearer is returned and the farther pushed.
 // Returns the next node to visit, or DK_NONE to pop.
-template <bool UNIT_TIME, int STACK, int BS>
+template <bool UNIT_TIME, int STACK>
 __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
                                              float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
                                              uint32_t& overflow) {
@@ -614,7 +613,7 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
     if (li && ri) {
         const bool lfirst = tl <= tr;
         if (sp < STACK) {
-            stk[sp * BS] = lfirst ? lr.y : lr.x;
+            stk[sp * BLOCK] = lfirst ? lr.y : lr.x;
             sp++;
         } else {
             overflow = 1;
@@ -631,31 +630,12 @@ __device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, co
 // and no second fetch), any other child a box slot.  Same contract as
 // bvh_step: the nearer hit inner child is returned, the farther pushed;
 // exact ties between leaves by the tie keys.
-// General kernels' LDS: tables (5 KB) | stack STACK x BS words | COLD x BS
-// words | the hot DNodes (DevScene::lnode, lnode_n)
-constexpr int COLD = 12;
-constexpr size_t gnode_lds_offset(int STACK, int BS) { return 4096 + 1024 + (size_t)(STACK + COLD) * BS * 4; }
-constexpr int GBLOCK_LDS = 1024;  // general kernels with a DNode window: one block per CU
-constexpr uint32_t gnode_lds_cap(int STACK) {  // DNodes that fit beside the stack and COLD (160 KB per CU)
-    return gnode_lds_offset(STACK, GBLOCK_LDS) >= 163840
-               ? 0u
-               : (uint32_t)((163840 - gnode_lds_offset(STACK, GBLOCK_LDS)) / sizeof(DNode));
-}
-extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-template <int STACK, int BS>
-__device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t ref, uint32_t idx, const Ray& r, const SlabRay& q, float a,
+template <int STACK>
+__device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
                                                float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
                                                uint32_t& overflow) {
-    float4 a0, a1, b0, b1;
-    const bool hot = (ref >> KIND_SHIFT) == DK_BVHL;
-    if (hot && S.lnode_n) {  // a hot node, in LDS
-        const float4* np = reinterpret_cast<const float4*>(smem + gnode_lds_offset(STACK, BS)) + 4 * idx;
-        a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
-    } else {
-        const float4* np = reinterpret_cast<const float4*>((hot ? S.lnode : S.node) + idx);
-        a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
-    }
+    const float4* np = reinterpret_cast<const float4*>(S.node + idx);
+    const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
     const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
     const float btc = cull_bound(bt);
     float ta = 0.0f, tb = 0.0f;
@@ -683,7 +663,7 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t ref, 
     if (ha && hb) {
         const bool afirst = ta <= tb;
         if (sp < STACK) {
-            stk[sp * BS] = afirst ? refb : refa;
+            stk[sp * BLOCK] = afirst ? refb : refa;
             sp++;
         } else {
             overflow = 1;
@@ -848,12 +828,12 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
 // when the ray scatters inside.  Draws 1 or 2 numbers, as the reference.
 // ANYB: media whose boundary needs the general traversal may occur (MB_ANY);
 // without them the kernel carries no nested traversal (fewer registers).
-template <bool MEDIA, int STACK, int BS, bool ANYB = true>
+template <bool MEDIA, int STACK, bool ANYB = true>
 __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin,
                                          float tmax, uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow,
                                          uint32_t prev, bool strict = false, Prof* prof = nullptr);
 
-template <int STACK, int BS, bool ANYB>
+template <int STACK, bool ANYB>
 __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, const Ray& wray,
                                            float tmin, float& bt, uint32_t* stk, int sp, Rng& rng, uint32_t& overflow) {
     const DMedium M = S.med[idx];
@@ -905,9 +885,9 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
         }
     } else if constexpr (ANYB) {
         Best b1, b2;
-        two = traverse<false, STACK, BS>(S, M.boundary, wray, M.chain, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow,
+        two = traverse<false, STACK>(S, M.boundary, wray, M.chain, -FLT_MAX, FLT_MAX, stk, sp, rng, b1, overflow,
                                      mkref(DK_NONE, 0)) &&
-              traverse<false, STACK, BS>(S, M.boundary, wray, M.chain, (float)((double)b1.t + 0.0001), FLT_MAX, stk, sp,
+              traverse<false, STACK>(S, M.boundary, wray, M.chain, (float)((double)b1.t + 0.0001), FLT_MAX, stk, sp,
                                      rng, b2, overflow, mkref(DK_NONE, 0));
         t1 = b1.t;
         t2 = b2.t;
@@ -937,7 +917,7 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
 // stk: this lane's LDS stack column.
 // `prev`: the leaf that holds tmax from before the call (DK_NONE: none), for
 // exact ties at tmax.
-template <bool MEDIA, int STACK, int BS, bool ANYB>
+template <bool MEDIA, int STACK, bool ANYB>
 __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin,
                                          float tmax, uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow,
                                          uint32_t prev, bool strict, Prof* prof) {
@@ -956,16 +936,16 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
         if (prof) {  // instrumented kernel only (a null pointer otherwise: folded away)
             prof->lane_steps++;
             if (first_active_lane()) prof->wave_steps++;
-            if (kind == DK_BVH || kind == DK_BVHL) prof->leaf_tests++;
+            if (kind == DK_BVH) prof->leaf_tests++;
         }
         const uint32_t idx = cur & INDEX_MASK;
-        if (kind == DK_BVH || kind == DK_BVHL) {
+        if (kind == DK_BVH) {
             const uint32_t before = best.prim;
             uint32_t b = before;
-            const uint32_t nxt = S.gnode ? dnode_step<STACK, BS>(S, cur, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
+            const uint32_t nxt = S.gnode ? dnode_step<STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
                                  : S.unit_time
-                                     ? bvh_step<true, STACK, BS>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
-                                     : bvh_step<false, STACK, BS>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow);
+                                     ? bvh_step<true, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
+                                     : bvh_step<false, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow);
             if (b != before) {
                 best.prim = b;
                 found = true;
@@ -1017,7 +997,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
             if ((item >> KIND_SHIFT) != DK_NONE) {
                 if ((S.refs[at + 1] >> KIND_SHIFT) != DK_NONE) {
                     if (sp < STACK) {
-                        stk[sp * BS] = mkref(DK_LISTNEXT, at + 1);
+                        stk[sp * BLOCK] = mkref(DK_LISTNEXT, at + 1);
                         sp++;
                     } else {
                         overflow = 1;
@@ -1034,7 +1014,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
             // constants of the innermost frame only
             const DInst& I = S.inst[idx];
             if (sp < STACK) {
-                stk[sp * BS] = mkref(DK_EXIT, I.parent_chain);
+                stk[sp * BLOCK] = mkref(DK_EXIT, I.parent_chain);
                 sp++;
                 r = apply_inst(S, cur, r);
                 cur = I.child;
@@ -1064,7 +1044,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                 float tin = bt;
                 if (kind == DK_PROGNEXT) {  // back from an item: its interval sits below the marker
                     --sp;
-                    tin = __uint_as_float(stk[sp * BS]);
+                    tin = __uint_as_float(stk[sp * BLOCK]);
                 }
                 bool descend = false;
                 while (true) {
@@ -1082,8 +1062,8 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                     // then on with the program
                     pos++;
                     if (sp + 2 <= STACK) {
-                        stk[sp * BS] = __float_as_uint(tin);
-                        stk[(sp + 1) * BS] = mkref(DK_PROGNEXT, pos);
+                        stk[sp * BLOCK] = __float_as_uint(tin);
+                        stk[(sp + 1) * BLOCK] = mkref(DK_PROGNEXT, pos);
                         sp += 2;
                         cur = w.w;
                         if ((cur >> KIND_SHIFT) == DK_MEDIUM) tmed = tin;
@@ -1101,7 +1081,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                 // program) its subtree's interval; the nearest record is kept
                 float tm = tmed == tmed ? tmed : bt;
                 tmed = __builtin_nanf("");
-                if (medium_hit<STACK, BS, ANYB>(S, idx, r, a, wray, tmin, tm, stk, sp, rng, overflow) &&
+                if (medium_hit<STACK, ANYB>(S, idx, r, a, wray, tmin, tm, stk, sp, rng, overflow) &&
                     (tm < bt || (tm == bt && wins_tie(S, cur, best.prim)))) {
                     bt = tm;
                     best.prim = cur;
@@ -1111,7 +1091,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
         }
         if (sp == sp0) break;
         --sp;
-        cur = stk[sp * BS];
+        cur = stk[sp * BLOCK];
     }
     best.t = bt;
     return found;
@@ -1122,7 +1102,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
 // hit so far.  The loop is uniform across the wave (see DTop).
 // MEDIA / ANYB: media below the top level (the general traversal asks them);
 // TOPMED: media as top-level items (TOP_MEDIUM).
-template <bool MEDIA, int STACK, int BS, bool ANYB, bool TOPMED, bool PROF = false>
+template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false>
 __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
                              uint32_t& overflow, bool strict, Prof* prof = nullptr) {
     float bt = FLT_MAX;
@@ -1147,7 +1127,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
         if (T.kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
             Best b;
-            if (traverse<MEDIA, STACK, BS, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp, strict,
+            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp, strict,
                                              PROF ? prof : nullptr)) {
                 bt = b.t;
                 bp = b.prim;
@@ -1190,7 +1170,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         } else if (TOPMED && T.kind == TOP_MEDIUM) {
             // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
             // so far as tmax, in the medium's frame; it draws as the reference
-            if (medium_hit<STACK, BS, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) {
+            if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) {
                 bp = mkref(DK_MEDIUM, T.a);
                 found = true;
             }
@@ -1654,9 +1634,10 @@ __device__ __forceinline__ float fx_value(unsigned long long q) { return (float)
 // (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
 // words: the path state the traversal does not read, parked while it runs
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
+constexpr int COLD = 12;
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
-    return general ? gnode_lds_offset(STACK, BS) + (size_t)n_node * sizeof(DNode)
-                   : 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0);
+    return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
+           (general ? (size_t)COLD * BS * 4 : 0);
 }
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
@@ -1666,6 +1647,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     unsigned long long t_mark = PROF ? __builtin_amdgcn_s_memtime() : 0;
     constexpr bool SIMPLE = MODE == 0;
     static_assert(STACK * 64 >= 640, "wave_turbulence scratch lives in the wave's stack columns");
+    static_assert(MODE == 0 || BS == BLOCK, "the general traversal strides its LDS stack by BLOCK");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* s_ranvec = reinterpret_cast<float4*>(smem);
     uint32_t* s_perm = reinterpret_cast<uint32_t*>(smem + 4096);
     uint32_t* s_stack = reinterpret_cast<uint32_t*>(smem + 5120);
@@ -1679,11 +1662,6 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         const float4* g = reinterpret_cast<const float4*>(S.node);
         for (uint32_t i = threadIdx.x; i < S.n_node * 4u; i += BS) s_node[i] = g[i];
         nodes = reinterpret_cast<const DNode*>(s_node);
-    }
-    if constexpr (!SIMPLE) {  // the general kernels' DNode window
-        float4* s_node = reinterpret_cast<float4*>(smem + gnode_lds_offset(STACK, BS));
-        const float4* g = reinterpret_cast<const float4*>(S.lnode);
-        for (uint32_t i = threadIdx.x; i < S.lnode_n * 4u; i += BS) s_node[i] = g[i];
     }
     __syncthreads();
     const Tables T{s_ranvec, s_perm};
@@ -1800,7 +1778,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                     prof.cyc_other += t_now - t_mark;
                     t_mark = t_now;
                 }
-                hit = traverse_top<MODE == 3 || MODE == 4, STACK, BS, MODE == 3, MODE >= 3, PROF>(S, ray, 0.001f, stk, rng,
+                hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF>(S, ray, 0.001f, stk, rng,
                                                                                            best, overflow, strict,
                                                                                            &prof);
                 if constexpr (PROF) {
@@ -2038,7 +2016,6 @@ struct HostLayout {
     std::vector<float> abox;         // DevScene::abox
     std::vector<DProg> prog;         // DevScene::prog
     std::vector<DBox6> box6;         // DevScene::box6
-    std::vector<DNode> lnode;        // DevScene::lnode (hotNodes)
     float tshift[3] = {0.0f, 0.0f, 0.0f};  // DevScene::tshift
 };
 
@@ -3233,107 +3210,6 @@ void buildGeneralNodes(HostLayout& L) {
     L.gnode = !L.bvh.empty();
 }
 
-// How often rays visit each DNode of a general scene, by the surface-area
-// model the SAH build itself uses: every top-level tree is entered by every
-// ray, and a child gets the share area(child box) / area(node box) of its
-// node's visits (instances and lists hand theirs on unchanged).  Reached nodes
-// only (in SAH mode the reference trees stay in the array, unvisited).  The
-// model ignores culling by the closest hit: it ranks nodes, it does not count
-// visits.
-std::vector<double> nodeHeat(const HostLayout& L) {
-    std::vector<double> P(L.node.size(), 0.0);
-    if (!L.gnode || L.node.empty()) return P;
-    size_t budget = 1u << 20;  // walk steps (a shared subtree is walked once per parent)
-    auto area = [](double dx, double dy, double dz) {
-        dx = std::max(0.0, dx), dy = std::max(0.0, dy), dz = std::max(0.0, dz);
-        return dx * dy + dy * dz + dz * dx;
-    };
-    auto slot_area = [&](const DBvh& b, int k) {
-        return area((double)b.xs[2 * k + 1] - b.xs[2 * k], (double)b.ys[2 * k + 1] - b.ys[2 * k],
-                    (double)b.zs[2 * k + 1] - b.zs[2 * k]);
-    };
-    auto node_area = [&](const DBvh& b) {  // the union of the two slots' boxes
-        auto ext = [](const float* v) { return (double)std::max(v[1], v[3]) - std::min(v[0], v[2]); };
-        return area(ext(b.xs), ext(b.ys), ext(b.zs));
-    };
-    std::function<void(uint32_t, double, int)> walk = [&](uint32_t ref, double p, int depth) {
-        if (depth > 256 || budget == 0 || !(p > 1e-12)) return;
-        budget--;
-        const uint32_t k = ref >> KIND_SHIFT, i = ref & INDEX_MASK;
-        switch (k) {
-        case DK_BVH: {
-            if (i >= L.bvh.size()) return;
-            P[i] += p;
-            const DBvh& b = L.bvh[i];
-            const double an = std::max(node_area(b), 1e-30);
-            walk(b.left, p * std::min(1.0, slot_area(b, 0) / an), depth + 1);
-            if (b.right != b.left) walk(b.right, p * std::min(1.0, slot_area(b, 1) / an), depth + 1);
-            break;
-        }
-        case DK_LIST:
-            for (uint32_t j = 0; j < L.list[i].count; j++) walk(L.refs[L.list[i].first + j], p, depth + 1);
-            break;
-        case DK_TRANSLATE:
-        case DK_ROTY:
-        case DK_FLIP:
-            walk(L.inst[i].child, p, depth + 1);
-            break;
-        case DK_MEDIUM:
-            walk(L.med[i].boundary, p, depth + 1);
-            break;
-        default:
-            break;
-        }
-    };
-    if (L.top.empty()) {
-        walk(L.root, 1.0, 0);
-    } else {
-        for (const DTop& t : L.top)
-            if (t.kind == TOP_GENERIC) walk(t.a, 1.0, 0);
-    }
-    return P;
-}
-
-// The `cap` hottest DNodes (nodeHeat) of a general scene in SAH mode become
-// DevScene::lnode: node i is referenced as DK_BVHL | slot from every DNode and
-// top-level item that pointed at it (the copies in lnode carry the rewritten
-// refs too), so a step knows from the ref alone where its node is; the
-// 1024-thread kernels hold lnode in LDS.  Nothing else changes: the DBvh array,
-// the tie keys and every other ref keep their indices.  Returns the modelled
-// share of the visits the hot nodes take.
-double hotNodes(HostLayout& L, uint32_t cap) {
-    L.lnode.clear();
-    if (!L.gnode || cap == 0) return 0.0;
-    const std::vector<double> P = nodeHeat(L);
-    std::vector<uint32_t> order;
-    double tot = 0;
-    for (uint32_t i = 0; i < P.size(); i++) {
-        tot += P[i];
-        if (P[i] > 0) order.push_back(i);
-    }
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return P[a] > P[b]; });
-    if (order.size() > cap) order.resize(cap);
-    std::sort(order.begin(), order.end());  // slots in node order (a tree's nodes stay together)
-    std::vector<uint32_t> slot(L.node.size(), ~0u);
-    double share = 0;
-    for (uint32_t k = 0; k < order.size(); k++) {
-        slot[order[k]] = k;
-        share += P[order[k]];
-    }
-    auto rw = [&](uint32_t& r) {
-        const uint32_t i = r & INDEX_MASK;
-        if ((r >> KIND_SHIFT) == DK_BVH && i < slot.size() && slot[i] != ~0u) r = mkref(DK_BVHL, slot[i]);
-    };
-    for (DNode& n : L.node) {
-        rw(n.ref_a);
-        rw(n.ref_b);
-    }
-    for (DTop& t : L.top)
-        if (t.kind == TOP_GENERIC) rw(t.a);
-    for (uint32_t i : order) L.lnode.push_back(L.node[i]);
-    return tot > 0 ? share / tot : 0.0;
-}
-
 bool textureNeedsUv(const rtow_scene& s, uint32_t ti, int guard = 0) {
     if (ti >= s.n_textures || guard > 32) return false;
     const rtow_texture& t = s.textures[ti];
@@ -3587,10 +3463,7 @@ int ensure(void** p, size_t* have, size_t need) {
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
-    DevScene sc = c->scene;
-    // the hot DNodes go to LDS in the 1024-thread kernels (others read them from memory)
-    if (MODE == 0 || BS != GBLOCK_LDS || sc.lnode_n > gnode_lds_cap(STACK)) sc.lnode_n = 0;
-    const size_t lds = lds_bytes(STACK, BS, MODE == 0 ? sc.n_node : sc.lnode_n, LDSN, MODE != 0);
+    const size_t lds = lds_bytes(STACK, BS, c->scene.n_node, LDSN, MODE != 0);
     // the occupancy query is host work between the launch events: once per
     // (kernel, LDS size) per process
     static std::mutex mu;
@@ -3612,7 +3485,7 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
     uint32_t grid = (uint32_t)c->cus * per;
     uint32_t maxUseful = (P.n_items + BS - 1) / BS;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
-    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>), dim3(grid), dim3(BS), lds, st, sc,
+    hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>), dim3(grid), dim3(BS), lds, st, c->scene,
                        cam, P,
                        (uint32_t*)c->d_work, c->fx_cur, (unsigned long long*)((uint8_t*)c->d_work + 8));
     HIP_TRY(hipGetLastError());
@@ -3624,11 +3497,7 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
 template <int MODE, int STACK>
 int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     if (c->dbg_out) return launchTrace<MODE, STACK, 1, false, BLOCK, false, true>(c, cam, P, bpc, st);
-    if constexpr (MODE != 0 && STACK <= 20) {  // one 1024-thread block per CU: room for the DNode window
-        if (c->profile) return launchTrace<MODE, STACK, 4, true, GBLOCK_LDS>(c, cam, P, bpc, st);
-        if (c->waves == 4) return launchTrace<MODE, STACK, 4, false, GBLOCK_LDS>(c, cam, P, bpc, st);
-    }
-    if constexpr (MODE != 0 && STACK > 20 && STACK <= 32) {
+    if constexpr (MODE != 0 && STACK <= 32) {
         if (c->profile) return launchTrace<MODE, STACK, 4, true>(c, cam, P, bpc, st);
     }
     if constexpr (STACK <= 32) {
@@ -3638,8 +3507,7 @@ int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
             if (c->lds_nodes && lds_bytes(STACK, 512, c->scene.n_node, true) <= 80 * 1024)
                 return launchTrace<MODE, STACK, 4, false, 512, true>(c, cam, P, bpc, st);
         }
-        if constexpr (MODE == 0 || STACK > 20)
-            if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
+        if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
         if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
         if constexpr (MODE == 0 || MODE == 2 || MODE == 3) {
             if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
@@ -3905,15 +3773,13 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
     int rc = buildLayout(*s, L);
     if (rc) return rc;
     if (L.stack_need > 64) return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
-    double hshare = 0;
-    if (!L.simple && L.stack_need <= 20) hshare = hotNodes(L, L.stack_need <= 16 ? gnode_lds_cap(16) : gnode_lds_cap(20));
     if (std::getenv("RTOW_LAYOUT_INFO"))
         std::fprintf(stderr,
                      "rtow-layout: simple %d gnode %d nodes %zu bvh %zu spheres %zu rects %zu lists %zu insts %zu media %zu "
-                     "top %zu stack_need %u chain_need %u media_nested %d media_any %d hot DNodes %zu (%.3f of the modelled visits)\n",
+                     "top %zu stack_need %u chain_need %u media_nested %d media_any %d\n",
                      (int)L.simple, (int)L.gnode, L.node.size(), L.bvh.size(), L.sph.size(), L.rect.size(), L.list.size(),
                      L.inst.size(), L.med.size(), L.top.size(), L.stack_need, L.chain_need, (int)L.media_nested,
-                     (int)L.media_any, L.lnode.size(), hshare);
+                     (int)L.media_any);
     if (stack_need) *stack_need = L.stack_need;
     if (chain_need) *chain_need = L.chain_need;
     return RTOW_OK;
@@ -3931,11 +3797,6 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     HostLayout L;
     int rc = buildLayout(*s, L, c->tree);
     if (rc) return rc;
-    // the hot DNodes, sized for the STACK launchStack will pick (16 or 20 entries)
-    if (c->lds_nodes && !L.simple && L.stack_need <= 20)
-        hotNodes(L, L.stack_need <= 16 ? gnode_lds_cap(16) : gnode_lds_cap(20));
-    const size_t n_hot = L.lnode.size();
-    if (L.lnode.empty()) L.lnode.push_back(DNode{});
     std::vector<uint8_t> blob;
     size_t o_bvh = pushBlob(blob, L.bvh), o_node = pushBlob(blob, L.node), o_sph = pushBlob(blob, L.sph);
     size_t o_rect = pushBlob(blob, L.rect), o_inst = pushBlob(blob, L.inst), o_list = pushBlob(blob, L.list);
@@ -3954,7 +3815,6 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_prog = pushBlob(blob, L.prog);
     if (L.box6.empty()) L.box6.push_back(DBox6{});
     size_t o_box6 = pushBlob(blob, L.box6);
-    size_t o_lnode = pushBlob(blob, L.lnode);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -4002,9 +3862,6 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.bvh_root = L.bvh_root;
     d.n_node = L.simple ? (uint32_t)L.node.size() : 0u;
     d.gnode = L.gnode ? 1u : 0u;
-    // the DNode window for the STACK launchStack will pick (16 or 20 entries)
-    d.lnode = (const DNode*)(b + o_lnode);
-    d.lnode_n = (uint32_t)n_hot;
     d.media_nested = L.media_nested ? 1u : 0u;
     c->has_scene = true;
     // progressive sums belong to the scene they were rendered from: a new

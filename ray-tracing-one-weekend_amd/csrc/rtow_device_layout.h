@@ -36,7 +36,6 @@ enum : uint32_t {
     DK_RECTS = 11,     // a list of rectangles only (a Box's sides): DList over rect[first, first+count)
     DK_PROG = 12,      // a BvhNode subtree holding media, visited as the reference visits it (DProg)
     DK_PROGNEXT = 13,  // traversal-stack marker: continue a DProg program at prog[index]
-    DK_BVHL = 14,      // a general scene's DNode held in LDS: DevScene::lnode[index]
     DK_NONE = 15
 };
 
@@ -242,13 +241,6 @@ struct DevScene {
     uint32_t n_node;         // DNode count (simple scenes)
     float tshift[3];         // simple scenes: world-frame offset of the DNode boxes (shiftBoxes)
     uint32_t gnode;          // general scene: node[i] is the DNode twin of bvh[i] (DK_BVH steps read it)
-    // general scene: the DNodes rays visit most (hotNodes), referenced as
-    // DK_BVHL | slot from the DNodes and top-level items; lnode[slot] is the
-    // node (its child refs rewritten alike).  The 1024-thread kernels copy
-    // the lnode_n entries into LDS at start; kernels without the room get
-    // lnode_n = 0 and read lnode from memory
-    const DNode* lnode;
-    uint32_t lnode_n;
 };
 
 }  // namespace rtow_dev
