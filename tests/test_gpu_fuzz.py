@@ -114,3 +114,53 @@ def test_gpu_matches_oracle_on_edited_worlds(case, gpu_ctx):
     assert np.isfinite(a).all()
     assert (rms <= 1e-4).all(), rms
     assert st.segments == oc.segments
+
+
+def _edit_spheres(d, rng):
+    """random_ned with every small sphere moved (up to half a unit), resized
+    (x0.5..1.5) and given another sphere's material, BVH boxes refreshed:
+    the simple-scene kernel (SAH rebuild or the reference tree as edited)"""
+    e = dict(d)
+    h = d["hitables"].copy()
+    sph = np.nonzero((h["kind"] == sio.HIT_SPHERE) | (h["kind"] == sio.HIT_MOVING_SPHERE))[0]
+    small = [int(i) for i in sph if (h[i]["f"][3] if h[i]["kind"] == sio.HIT_SPHERE else h[i]["f"][8]) < 0.5]
+    mats = h["a"][small].copy()
+    rng.shuffle(mats)
+    for i, m in zip(small, mats):
+        off = rng.uniform(-0.5, 0.5, 3).astype(np.float32)
+        off[2] = 0.0  # NED: z is down; keep them on the ground plane's side
+        h[i]["f"][:3] += off
+        if h[i]["kind"] == sio.HIT_MOVING_SPHERE:
+            h[i]["f"][3:6] += off
+            h[i]["f"][8] *= np.float32(rng.uniform(0.5, 1.5))
+        else:
+            h[i]["f"][3] *= np.float32(rng.uniform(0.5, 1.5))
+        h[i]["a"] = m
+    e["hitables"] = h
+    sio.refresh_bvh_boxes(e)
+    return e
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_gpu_matches_oracle_on_edited_random_scenes(case, gpu_ctx):
+    rng = np.random.default_rng(2000 + case)
+    d = sio.scene_dict(rtow.Scene.build("random_ned", n=100, image="synthetic"))
+    arr = sio.ArrayScene(_edit_spheres(d, rng))
+    assert rtow.lib().rtow_scene_check(arr.view_ptr, None, None) == rtow.OK
+    W, H = 48, 32
+    cam = rtow.camera_main(W, H) if case % 2 == 0 else _camera(W, H, rng, 2.0)
+    p = rtow.params(W, H, 8, seed=70 + case)
+    tree = "reference" if case % 4 >= 2 else "sah"
+    gpu_ctx.set_tree(tree)
+    try:
+        gpu_ctx.upload(arr)
+        _, lin, st = gpu_ctx.render(cam, p)
+    finally:
+        gpu_ctx.set_tree("sah")
+    olin, _, oc = sio.oracle_render(arr.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p)))
+    a = np.asarray(lin, np.float64).reshape(-1, 3)
+    rms = np.sqrt(np.mean((a - olin.astype(np.float64)) ** 2, axis=0))
+    print(f"FUZZ-SIMPLE {case} {tree}: rms {rms} segments gpu {st.segments} oracle {oc.segments}")
+    assert (rms <= 1e-4).all(), rms
+    assert st.segments == oc.segments
