@@ -351,6 +351,20 @@ int rtow_render_tiles_device(rtow_context* ctx, const rtow_camera* cam, const rt
                              void* d_bgra_slab, void* d_linear_slab, void* stream,
                              rtow_stats* stats);
 
+/* Progressive rendering over this rank's tiles (p->rank of p->world): the
+ * multi-GPU form of rtow_render_progressive.  Each call adds p->spp new samples
+ * per pixel of the rank's tiles to the context's running sums (restarted as
+ * rtow_render_progressive's are, and also when rank or world change) and
+ * writes the average so far into DEVICE slabs laid out as
+ * rtow_render_tiles_device's, ready for one gather and rtow_assemble_device.
+ * The assembled frame of every rank's call equals rtow_render_progressive's
+ * frame of the same calls bit for bit (the RNG is keyed by global pixel).
+ * Enqueued on `stream` (NULL = the context's own); returns after the work
+ * completes. */
+int rtow_render_progressive_tiles_device(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
+                                         int reset, void* d_bgra_slab, void* d_linear_slab, void* stream,
+                                         uint32_t* total_spp, rtow_stats* stats);
+
 /* Diagnostic: render the frame with the segment-recording kernel and return
  * the path of ONE sample (pixel x, y of the top-down frame, sample index):
  * per color() call RTOW_DEBUG_SEG_FLOATS floats {hit, depth, t, p.xyz (the

@@ -3891,12 +3891,15 @@ int rtow_render(rtow_context* c, const rtow_camera* cam, const rtow_params* p, u
     return RTOW_OK;
 }
 
-int rtow_render_progressive(rtow_context* c, const rtow_camera* cam, const rtow_params* p, int reset,
-                            uint8_t* bgra_out, float* linear_out, uint32_t* total_spp, rtow_stats* stats) {
-    if (!c || !p || !cam) return set_error(RTOW_E_INVALID, "NULL argument");
-    rtow_params q = *p;
-    q.rank = 0;
-    q.world = 1;
+}  // extern "C"
+
+namespace {
+// The running sums of rtow_render_progressive / rtow_render_progressive_tiles_device:
+// q->rank of q->world's pixels (one rank: the whole frame); the average so far
+// goes to the slabs (tiles) or the frame buffers (whole frame), both device.
+int progressiveCore(rtow_context* c, const rtow_camera* cam, const rtow_params& q, int reset, uint8_t* slab_bgra,
+                    float* slab_lin, uint8_t* fb_bgra, float* fb_lin, hipStream_t st, uint32_t* total_spp,
+                    rtow_stats* stats) {
     // what the accumulated samples were rendered with: camera + every param but spp / chunking
     rtow_params key = q;
     key.spp = 0;
@@ -3911,26 +3914,44 @@ int rtow_render_progressive(rtow_context* c, const rtow_camera* cam, const rtow_
         c->accum_sig = sig;
     }
     if ((uint64_t)c->accum_spp + q.spp > 0xffffffffull) return set_error(RTOW_E_INVALID, "too many accumulated samples");
+    const uint32_t world = q.world ? q.world : 1;
+    if (q.rank >= world) return set_error(RTOW_E_INVALID, "rank >= world");
     HIP_TRY(hipSetDevice(c->device));
-    const size_t npx = (size_t)q.width * q.height;
-    size_t need = npx * 4 + npx * 12 + 256;
-    int rc = ensure((void**)&c->d_fb, &c->fb_bytes, need);
-    if (rc) return rc;
-    const size_t acc_need = (size_t)rtow_rank_tile_count(q.width, q.height, 0, 1) * 64 * 4 * sizeof(unsigned long long);
+    const size_t acc_need = (size_t)rtow_rank_tile_count(q.width, q.height, q.rank, world) * 64 * 4 *
+                            sizeof(unsigned long long);
     if (c->accum_bytes < acc_need) c->accum_spp = 0;
-    rc = ensure((void**)&c->d_accum, &c->accum_bytes, acc_need);
+    int rc = ensure((void**)&c->d_accum, &c->accum_bytes, acc_need);
     if (rc) return rc;
-    if (c->accum_spp == 0) HIP_TRY(hipMemsetAsync(c->d_accum, 0, acc_need, c->stream));
-    uint8_t* d_bgra = c->d_fb;
-    float* d_lin = (float*)(c->d_fb + ((npx * 4 + 255) & ~size_t(255)));
-    rc = renderCore(c, cam, &q, nullptr, nullptr, d_bgra, linear_out ? d_lin : nullptr, c->stream, stats, c->d_accum,
-                    c->accum_spp);
+    if (c->accum_spp == 0) HIP_TRY(hipMemsetAsync(c->d_accum, 0, acc_need, st));
+    rc = renderCore(c, cam, &q, slab_bgra, slab_lin, fb_bgra, fb_lin, st, stats, c->d_accum, c->accum_spp);
     if (rc) {
         c->accum_spp = 0;
         return rc;
     }
     c->accum_spp += q.spp;
     if (total_spp) *total_spp = c->accum_spp;
+    return RTOW_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rtow_render_progressive(rtow_context* c, const rtow_camera* cam, const rtow_params* p, int reset,
+                            uint8_t* bgra_out, float* linear_out, uint32_t* total_spp, rtow_stats* stats) {
+    if (!c || !p || !cam) return set_error(RTOW_E_INVALID, "NULL argument");
+    rtow_params q = *p;
+    q.rank = 0;
+    q.world = 1;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t npx = (size_t)q.width * q.height;
+    size_t need = npx * 4 + npx * 12 + 256;
+    int rc = ensure((void**)&c->d_fb, &c->fb_bytes, need);
+    if (rc) return rc;
+    uint8_t* d_bgra = c->d_fb;
+    float* d_lin = (float*)(c->d_fb + ((npx * 4 + 255) & ~size_t(255)));
+    rc = progressiveCore(c, cam, q, reset, nullptr, nullptr, d_bgra, linear_out ? d_lin : nullptr, c->stream, total_spp,
+                         stats);
+    if (rc) return rc;
     if (bgra_out) HIP_TRY(hipMemcpy(bgra_out, d_bgra, npx * 4, hipMemcpyDeviceToHost));
     if (linear_out) HIP_TRY(hipMemcpy(linear_out, d_lin, npx * 12, hipMemcpyDeviceToHost));
     return RTOW_OK;
@@ -3970,6 +3991,17 @@ int rtow_render_tiles_device(rtow_context* c, const rtow_camera* cam, const rtow
     if (!c) return set_error(RTOW_E_INVALID, "NULL context");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return renderCore(c, cam, p, (uint8_t*)d_bgra_slab, (float*)d_linear_slab, nullptr, nullptr, st, stats);
+}
+
+int rtow_render_progressive_tiles_device(rtow_context* c, const rtow_camera* cam, const rtow_params* p, int reset,
+                                         void* d_bgra_slab, void* d_linear_slab, void* stream, uint32_t* total_spp,
+                                         rtow_stats* stats) {
+    if (!c || !p || !cam) return set_error(RTOW_E_INVALID, "NULL argument");
+    rtow_params q = *p;
+    if (q.world == 0) q.world = 1;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return progressiveCore(c, cam, q, reset, (uint8_t*)d_bgra_slab, (float*)d_linear_slab, nullptr, nullptr, st,
+                           total_spp, stats);
 }
 
 int rtow_assemble_device(rtow_context* c, uint32_t width, uint32_t height, uint32_t world, const void* d_slabs,

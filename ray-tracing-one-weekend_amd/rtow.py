@@ -115,6 +115,8 @@ def lib():
         "rtow_render": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)], i32),
         "rtow_render_tiles_device": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, vp,
                                       ctypes.POINTER(Stats)], i32),
+        "rtow_render_progressive_tiles_device": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), i32, vp, vp,
+                                                  vp, ctypes.POINTER(u32), ctypes.POINTER(Stats)], i32),
         "rtow_assemble_device": ([vp, u32, u32, u32, vp, u32, vp, vp], i32),
         "rtow_image_decode_jpeg": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp), ctypes.POINTER(u32),
                                     ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
@@ -384,6 +386,17 @@ class Context:
         check(lib().rtow_render_tiles_device(self._h, ctypes.byref(cam), ctypes.byref(p), d_bgra_slab, d_lin_slab,
                                              stream, ctypes.byref(st)), "rtow_render_tiles_device")
         return st
+
+    def render_progressive_tiles_device(self, cam, p, d_bgra_slab, d_lin_slab=None, reset=False, stream=None):
+        """rtow_render_progressive_tiles_device on device pointers (ints): p.spp new
+        samples of rank p.rank's tiles added to the running sums, the average so far
+        written to the slabs; returns (total spp, Stats)."""
+        total = ctypes.c_uint32()
+        st = Stats()
+        check(lib().rtow_render_progressive_tiles_device(self._h, ctypes.byref(cam), ctypes.byref(p), 1 if reset else 0,
+                                                         d_bgra_slab, d_lin_slab, stream, ctypes.byref(total),
+                                                         ctypes.byref(st)), "rtow_render_progressive_tiles_device")
+        return total.value, st
 
     def assemble_device(self, width, height, world, d_slabs, stride_px, d_frame, stream=None):
         check(lib().rtow_assemble_device(self._h, width, height, world, d_slabs, stride_px, d_frame, stream),

@@ -87,3 +87,58 @@ def test_progressive_restarts_on_scene_upload(gpu_ctx):
     assert total == 4
     _, one, _ = gpu_ctx.render(cam, p)
     assert np.array_equal(lin.view(np.uint32), one.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_progressive_tiles_assemble_to_progressive_frame(world, gpu_ctx):
+    """Multi-GPU progressive frames: every rank (its own context, as on its own
+    GPU) adds F frames of S spp of its tiles (rtow_render_progressive_tiles_device);
+    the assembled BGRA and linear frames equal rtow_render_progressive's after
+    the same F calls, bit for bit."""
+    import torch
+
+    W, H, S, F = 61, 45, 4, 3
+    scene = rtow.Scene.build("random_ned", n=100, image="synthetic")
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_main(W, H)
+    for f in range(F):
+        ref_bgra, ref_lin, _, _ = gpu_ctx.render_progressive(cam, rtow.params(W, H, S, seed=5), reset=(f == 0))
+    stride = rtow.rank_tile_count(W, H, 0, world) * 64
+    bgra = torch.zeros((world, stride * 4), dtype=torch.uint8, device="cuda")
+    lin = torch.zeros((world, stride * 3), dtype=torch.float32, device="cuda")
+    ctxs = [rtow.Context(0) for _ in range(world)]
+    try:
+        for r, ctx in enumerate(ctxs):
+            ctx.upload(scene)
+            for f in range(F):
+                total, _ = ctx.render_progressive_tiles_device(cam, rtow.params(W, H, S, seed=5, rank=r, world=world),
+                                                               bgra[r].data_ptr(), lin[r].data_ptr(), reset=(f == 0))
+                assert total == (f + 1) * S
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    fb = rtow.assemble(bgra.cpu().numpy().reshape(world, stride, 4), W, H, world)
+    fl = rtow.assemble(lin.cpu().numpy().reshape(world, stride, 3), W, H, world)
+    assert np.array_equal(fb, ref_bgra)
+    assert np.array_equal(fl.view(np.uint32), ref_lin.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_progressive_tiles_restart_on_partition_change(gpu_ctx):
+    """The running sums belong to one rank's tiles: a call for another rank or
+    world restarts them."""
+    import torch
+
+    W, H, S = 40, 24, 4
+    gpu_ctx.upload(rtow.Scene.build("three_sphere"))
+    cam = rtow.camera_main(W, H)
+    slab = torch.zeros(rtow.rank_tile_count(W, H, 0, 2) * 64 * 4, dtype=torch.uint8, device="cuda")
+    total, _ = gpu_ctx.render_progressive_tiles_device(cam, rtow.params(W, H, S, rank=0, world=2), slab.data_ptr(),
+                                                       reset=True)
+    total, _ = gpu_ctx.render_progressive_tiles_device(cam, rtow.params(W, H, S, rank=0, world=2), slab.data_ptr())
+    assert total == 2 * S
+    total, _ = gpu_ctx.render_progressive_tiles_device(cam, rtow.params(W, H, S, rank=1, world=2), slab.data_ptr())
+    assert total == S
+    with pytest.raises(rtow.RtowError):
+        gpu_ctx.render_progressive_tiles_device(cam, rtow.params(W, H, S, rank=2, world=2), slab.data_ptr())
