@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     args = ap.parse_args()
     torch.cuda.init()
-    threads = min(16, os.cpu_count() or 1)
+    threads, _ = rtow.host_threads()  # the CPUs this process may use (affinity, cgroup quota)
     ctx = rtow.Context(0)
     lines = []
     for k in [int(v) for v in args.configs.split(",")]:

@@ -31,7 +31,7 @@ def main():
     import torch
 
     torch.cuda.init()
-    threads = min(16, os.cpu_count() or 1)
+    threads, _ = rtow.host_threads()  # the CPUs this process may use (affinity, cgroup quota)
     ctx = rtow.Context(0)
     lines = []
     cases = [c for c in CASES if args.scenes is None or c[0] in args.scenes.split(",")]
