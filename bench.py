@@ -1,25 +1,36 @@
 #!/usr/bin/env python3
-"""Benchmark: BASELINE.json config 2 -- the book-1 random scene
+"""Benchmark of the per-pixel render loop (main.cpp:932-996) on N MI355X.
+
+Default workload: BASELINE.json config 2 -- the book-1 random scene
 (randomScene_NED with n = 487, 488 hitables under one BvhNode) at
-1920x1080x1024spp, depth 50, on N MI355X.
+1920x1080x1024spp, depth 50.  `--workload final_ned` is config 5 (book-2
+final_scene, 4096x4096x8192spp, quoted for 8 GPUs); cornell / cornell_smoke
+are configs 3 / 4.
 
 One step = one full frame: every rank renders its share of the frame's 8x8
-tiles (rank r takes tiles r, r+N, ...) with the HIP path in librtow_hip.so,
-then one RCCL gather (torch.distributed, backend "nccl") brings the tile
-slabs to rank 0, which assembles the BGRA frame on its GPU.  Total work is
-the fixed frame, so scaling is "strong".
+tiles (rank r takes tiles r, r+N, ...; the reference's column interleave,
+main.cpp:936, at tile granularity) with the HIP path in librtow_hip.so, then
+one RCCL gather (torch.distributed, backend "nccl") brings the tile slabs to
+rank 0, which assembles the BGRA frame on its GPU.  Total work is the fixed
+frame, so scaling is "strong".
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--spp S] [--no-cpu]
-  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--spp S] [--no-cpu]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
       --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line (value = whole-job Mray/s; Msample/s beside it).
+`--gpus N > 1` without a torch.distributed environment (WORLD_SIZE unset)
+starts N ranks itself (a torch.distributed.run child, before this process
+touches a GPU) and exits with its status; a WORLD_SIZE that differs from
+--gpus is an error.  A multi-GPU request never silently runs one rank.
+
+Rank 0 prints ONE JSON line (value = whole-job Mray/s; Msample/s beside it;
+`rank_kernel_ms` the trace kernel's time on every rank).
 
 roofline: the bound that limits this kernel is VALU issue, not HBM (the scene
 is LDS/L2-resident; measured HBM traffic is ~7 GB/s).  achieved = VALU
 wave-instructions per second of the trace kernel = (wave-instructions per ray,
 SQ_INSTS_VALU from the committed rocprofv3 PMC pass of this exact build and
-config, profiles/<round>_*/pmc_summary.json) x the rays this launch traced /
+workload, profiles/<round>_*/pmc_summary.json) x the rays this launch traced /
 the kernel's mean duration from HIP events on the render stream.  peak = 1024
 SIMDs x 2.4 GHz x 0.5 (a wave64 VALU instruction occupies a SIMD-32 for two
 cycles, MI355X_MICROARCH.md).  lane_util = the active-lane fraction of those
@@ -30,12 +41,15 @@ WRITE_SIZE of the same PMC run) and the reference-equivalent record bytes per
 ray are informational fields.  cpu_baseline = the reference's
 own code (oracle/_ref/ref_harness) on all the host cores this process may use
 over a bounded random pixel sample, rays counted by the C oracle on the same
-pixels (the oracle alone, kind "port", when the harness was not built).
+pixels (the oracle alone, kind "port", when the harness was not built);
+`as_written` beside it times the reference with its own shared, racy
+std::mt19937_64 (rngs.h:9-11).
 """
 import argparse
-import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -53,36 +67,81 @@ VALU_PEAK_G = N_SIMD * CLOCK_GHZ * 0.5
 # algorithmic record bytes per reference traversal event
 BYTES_BVH, BYTES_SPHERE, BYTES_MSPHERE, BYTES_RECT, BYTES_MEDIUM = 32, 20, 40, 24, 8
 
+# BASELINE.json configs by name: scene, n, W, H, spp, the world the config is quoted for, label
+WORKLOADS = {
+    "random_ned": ("random_ned", 487, 1920, 1080, 1024, "book-1 random_scene"),
+    "cornell": ("cornell", 0, 800, 800, 4096, "cornell_box"),
+    "cornell_smoke": ("cornell_smoke", 0, 800, 800, 4096, "cornell_smoke"),
+    "final_ned": ("final_ned", 0, 4096, 4096, 8192, "book-2 final_scene"),
+}
+BASELINE_METRIC = "Mray/s + Msample/s, random_scene 1920×1080×1024spp at 1/2/4/8 MI355X"
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=1024)
-    ap.add_argument("--n", type=int, default=487)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="random_ned")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-pixels", type=int, default=40000)
-    ap.add_argument("--cpu-spp", type=int, default=1024)
+    ap.add_argument("--cpu-pixels", type=int, default=None,
+                    help="pixels of the CPU baseline's sample (default: ~10-20 s of the reference's work)")
+    ap.add_argument("--cpu-spp", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-kind", choices=["auto", "port"], default="auto",
                     help="auto: the reference's own code when oracle/_ref was built, else the oracle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every host CPU this process may use")
     ap.add_argument("--pmc-json", default=None,
                     help="PMC summary to use (default: the newest profiles/*/pmc_summary.json of this build+config)")
-    return ap.parse_args()
+    args = ap.parse_args(argv)
+    scene, n, W, H, spp, _ = WORKLOADS[args.workload]
+    args.scene = scene
+    args.n = n if args.n is None else args.n
+    args.width = W if args.width is None else args.width
+    args.height = H if args.height is None else args.height
+    args.spp = spp if args.spp is None else args.spp
+    if args.cpu_spp is None:
+        args.cpu_spp = min(args.spp, 1024)
+    if args.cpu_pixels is None:  # ~10-20 s of the reference's code on 16 host cores
+        args.cpu_pixels = {"random_ned": 40000, "cornell": 8000, "cornell_smoke": 8000, "final_ned": 3000}[args.workload]
+    return args
 
 
-def reference_run(pix, args, threads):
+# ---------------------------------------------------------------------------
+# launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(nproc, argv, script=None):
+    """Start `nproc` ranks of `script` (default: this file) with argv through a
+    torch.distributed.run child on 127.0.0.1 and return its exit status.  The
+    caller must not have touched a GPU (the child, not an exec, runs them)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(script or __file__)] + list(argv)
+    return subprocess.run(cmd).returncode
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline
+def reference_run(pix, args, threads, racy=False):
     """The reference's own code (oracle/_ref/ref_harness, compiled from
     /root/reference's headers in the build container; its render loop body is
     main.cpp:938-951) on the same pixels: (seconds, checksum) or None when the
-    harness was not built.  The random scene loads its earth texture from
-    ./input_images/1_earth_8k.jpg (scenes.h:140): the synthetic texture the GPU
-    uses is staged there as a lossless PNG."""
-    import subprocess
+    harness was not built.  racy: with the reference's own shared
+    std::mt19937_64 (rngs.h:9-11) instead of the seeded counter engine.  The
+    scenes load their earth texture from ./input_images/1_earth_8k.jpg
+    (scenes.h:140): the synthetic texture the GPU uses is staged there as a
+    lossless PNG."""
     import tempfile
 
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
@@ -101,71 +160,14 @@ def reference_run(pix, args, threads):
         pf = os.path.join(d, "pix.u32")
         pix.tofile(pf)
         env = dict(os.environ, RTOW_SCENE_SEED="1")
-        out = subprocess.run([harness, "bench", "random_ned", str(args.width), str(args.height), str(args.cpu_spp), pf,
-                              "--n", str(args.n), "--seed", str(args.seed), "--threads", str(threads), "--cwd", d],
-                             env=env, capture_output=True, text=True, timeout=600)
+        cmd = [harness, "bench", args.scene, str(args.width), str(args.height), str(args.cpu_spp), pf,
+               "--n", str(max(args.n, 1)), "--seed", str(args.seed), "--threads", str(threads), "--cwd", d]
+        out = subprocess.run(cmd + (["--racy"] if racy else []), env=env, capture_output=True, text=True,
+                             timeout=600)
     if out.returncode != 0:
         return None
     r = json.loads(out.stdout.strip().splitlines()[-1])
     return r["seconds"], r["checksum"]
-
-
-def find_pmc(args, world, src_hash):
-    """The PMC summary (tools/profile_bench.sh) that describes this run: the
-    newest one under profiles/ recorded for this config and this build's
-    source hash; failing that the newest for this config, flagged stale."""
-    import glob
-
-    cands = [args.pmc_json] if args.pmc_json else sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.json")))
-    want = [args.width, args.height, args.spp, args.n, world]
-    fresh, stale = None, None
-    for f in cands:
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        if d.get("config") != want or "SQ_INSTS_VALU" not in d:
-            continue
-        if d.get("source_hash") == src_hash:
-            fresh = (f, d)
-        else:
-            stale = (f, d)
-    return fresh or stale
-
-
-def roofline(args, world, launch_rays, mean_kms, bpr, src_hash):
-    """VALU-issue roofline of the trace kernel (see the module docstring)."""
-    found = find_pmc(args, world, src_hash)
-    if found is None:
-        return {"bound": "valu", "achieved": None, "peak": VALU_PEAK_G, "unit": "Gwave-instr/s", "frac": None,
-                "traffic": None, "kernel_ms": round(mean_kms, 2), "note": "no PMC summary for this config under profiles/"}
-    path, d = found
-    rays_pmc = d["rays_per_launch"]
-    valu_per_ray = d["SQ_INSTS_VALU"] / rays_pmc
-    achieved = valu_per_ray * launch_rays / (mean_kms * 1e-3) / 1e9
-    lane_util = d["SQ_THREAD_CYCLES_VALU"] / (d["SQ_ACTIVE_INST_VALU"] * 64) if "SQ_THREAD_CYCLES_VALU" in d else None
-    traffic = None
-    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:  # KB; FETCH_SIZE reads half the bytes on gfx950
-        traffic = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024 / rays_pmc * launch_rays
-    frac = achieved / VALU_PEAK_G
-    roof = {"bound": "valu", "achieved": round(achieved, 1), "peak": VALU_PEAK_G, "unit": "Gwave-instr/s",
-            "frac": round(frac, 4),
-            "lane_util": round(lane_util, 4) if lane_util is not None else None,
-            "useful_lane_frac": round(frac * lane_util, 4) if lane_util is not None else None,
-            "traffic": round(traffic) if traffic is not None else None,
-            "valu_per_ray": round(valu_per_ray, 3), "kernel_ms": round(mean_kms, 2),
-            "pmc": os.path.relpath(path, REPO), "pmc_source_hash": d.get("source_hash"),
-            "pmc_matches_build": d.get("source_hash") == src_hash,
-            "peak_def": f"{N_SIMD} SIMD-32 x {CLOCK_GHZ} GHz x 0.5 wave64 VALU instr/cycle"}
-    if "GRBM_GUI_ACTIVE" in d and d.get("kernel_ms_pmc"):
-        roof["clock_ghz_under_pmc"] = round(d["GRBM_GUI_ACTIVE"] / 8 / (d["kernel_ms_pmc"] * 1e-3) / 1e9, 3)
-    if traffic is not None:
-        roof["hbm_gbps"] = round(traffic / (mean_kms * 1e-3) / 1e9, 2)
-        roof["hbm_frac"] = round(traffic / (mean_kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)
-    if bpr is not None:
-        roof["reference_bytes_per_ray"] = round(bpr, 1)
-        roof["reference_equiv_gbps"] = round(bpr * launch_rays / (mean_kms * 1e-3) / 1e9, 1)
-    return roof
 
 
 def cpu_baseline(scene, cam, args, threads):
@@ -201,6 +203,16 @@ def cpu_baseline(scene, cam, args, threads):
                 "sample": sample + ", oracle/_ref/ref_harness (the reference's headers); rays counted by the oracle",
                 "same_result_as_oracle": bool(abs(checksum - osum) <= 1e-6 * max(1.0, abs(osum))),
                 "port": {k: port[k] for k in ("value", "msample_per_s", "seconds")}}
+        racy = reference_run(pix, args, threads, racy=True)
+        if racy is not None:
+            # its paths differ from the seeded ones (other random numbers):
+            # rays estimated from the oracle's rays per sample on the same pixels
+            base["as_written"] = {
+                "value": round(c.segments / racy[0] / 1e6, 3), "unit": "Mray/s",
+                "msample_per_s": round(c.samples / racy[0] / 1e6, 4), "seconds": round(racy[0], 2),
+                "note": "the reference as written: every thread draws from the one shared std::mt19937_64 "
+                        "(rngs.h:9-11, main.cpp:942-943) unsynchronised -- a data race, so not reproducible; "
+                        "rays = samples x the seeded run's rays per sample"}
     counts = {"segments_per_sample": c.segments / max(c.samples, 1),
               "bvh_visits_per_ray": c.bvh_visits / max(c.segments, 1),
               "sphere_tests_per_ray": c.sphere_tests / max(c.segments, 1),
@@ -208,6 +220,81 @@ def cpu_baseline(scene, cam, args, threads):
     return base, bytes_per_ray, counts
 
 
+# ---------------------------------------------------------------------------
+# roofline
+def pmc_key(args, world):
+    """What a PMC summary must describe to price this run."""
+    return {"workload": args.scene, "config": [args.width, args.height, args.spp, args.n, world]}
+
+
+def find_pmc(args, world, src_hash):
+    """The PMC summary (tools/profile_bench.sh) that describes this run: the
+    newest one under profiles/ recorded for this workload, config and build
+    source hash; failing that the newest for this workload and config, flagged
+    stale.  "Newest" is the summary's own `created` stamp (unix seconds, from
+    tools/pmc_summarize.py), then the file's mtime."""
+    import glob
+
+    cands = [args.pmc_json] if args.pmc_json else glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.json"))
+    want = pmc_key(args, world)
+    fresh, stale = [], []
+    for f in cands:
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload", "random_ned") != want["workload"] or d.get("config") != want["config"]:
+            continue
+        if "SQ_INSTS_VALU" not in d:
+            continue
+        age = (d.get("created", 0), os.path.getmtime(f))
+        (fresh if d.get("source_hash") == src_hash else stale).append((age, f, d))
+    for group in (fresh, stale):
+        if group:
+            _, f, d = max(group, key=lambda e: e[0])
+            return f, d
+    return None
+
+
+def roofline(args, world, launch_rays, mean_kms, bpr, src_hash):
+    """VALU-issue roofline of the trace kernel (see the module docstring)."""
+    found = find_pmc(args, world, src_hash)
+    if found is None:
+        return {"bound": "valu", "achieved": None, "peak": VALU_PEAK_G, "unit": "Gwave-instr/s", "frac": None,
+                "traffic": None, "kernel_ms": round(mean_kms, 2), "note": "no PMC summary for this config under profiles/"}
+    path, d = found
+    rays_pmc = d["rays_per_launch"]
+    valu_per_ray = d["SQ_INSTS_VALU"] / rays_pmc
+    achieved = valu_per_ray * launch_rays / (mean_kms * 1e-3) / 1e9
+    lane_util = d["SQ_THREAD_CYCLES_VALU"] / (d["SQ_ACTIVE_INST_VALU"] * 64) if "SQ_THREAD_CYCLES_VALU" in d else None
+    traffic = None
+    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:  # KB; FETCH_SIZE reads half the bytes on gfx950
+        traffic = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024 / rays_pmc * launch_rays
+    frac = achieved / VALU_PEAK_G
+    roof = {"bound": "valu", "achieved": round(achieved, 1), "peak": VALU_PEAK_G, "unit": "Gwave-instr/s",
+            "frac": round(frac, 4),
+            "lane_util": round(lane_util, 4) if lane_util is not None else None,
+            "useful_lane_frac": round(frac * lane_util, 4) if lane_util is not None else None,
+            "traffic": round(traffic) if traffic is not None else None,
+            "valu_per_ray": round(valu_per_ray, 3), "kernel_ms": round(mean_kms, 2),
+            "pmc": os.path.relpath(path, REPO), "pmc_source_hash": d.get("source_hash"),
+            "pmc_matches_build": d.get("source_hash") == src_hash,
+            "peak_def": f"{N_SIMD} SIMD-32 x {CLOCK_GHZ} GHz x 0.5 wave64 VALU instr/cycle"}
+    if "WRITE_SIZE" in d:
+        roof["write_bytes"] = round(d["WRITE_SIZE"] * 1024 / rays_pmc * launch_rays)
+    if "GRBM_GUI_ACTIVE" in d and d.get("kernel_ms_pmc"):
+        roof["clock_ghz_under_pmc"] = round(d["GRBM_GUI_ACTIVE"] / 8 / (d["kernel_ms_pmc"] * 1e-3) / 1e9, 3)
+    if traffic is not None:
+        roof["hbm_gbps"] = round(traffic / (mean_kms * 1e-3) / 1e9, 2)
+        roof["hbm_frac"] = round(traffic / (mean_kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)
+    if bpr is not None:
+        roof["reference_bytes_per_ray"] = round(bpr, 1)
+        roof["reference_equiv_gbps"] = round(bpr * launch_rays / (mean_kms * 1e-3) / 1e9, 1)
+    return roof
+
+
+# ---------------------------------------------------------------------------
+# one step
 def frame_step(render, assemble, slab, gathered, rank, world, dist=None):
     """One bench step: this rank renders its 8x8-tile slab (`render(slab)`),
     one gather brings every rank's slab to rank 0 (torch.distributed: RCCL
@@ -223,110 +310,172 @@ def frame_step(render, assemble, slab, gathered, rank, world, dist=None):
     return st
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+class HipRank:
+    """One rank of the product path: librtow_hip.so on cuda:LOCAL_RANK, RCCL
+    (torch.distributed backend "nccl") between ranks."""
 
-    import rtow
+    backend = "nccl"
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    distributed = world > 1
-    if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    def __init__(self, args, rank, world, local):
+        import torch
 
-    def barrier():
-        if distributed:
-            dist.barrier()
+        import rtow
 
-    W, H, spp = args.width, args.height, args.spp
-    scene = rtow.Scene.build("random_ned", n=args.n, image="synthetic", scene_seed=1)
-    cam = rtow.camera_main(W, H)
-    ctx = rtow.Context(local)
-    ctx.upload(scene)
-    stride = rtow.rank_tile_count(W, H, 0, world) * 64  # rank 0 holds the most tiles
-    slab = torch.zeros(stride * 4, dtype=torch.uint8, device="cuda")
-    gathered = torch.zeros((world, stride * 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
-    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
-    stream = torch.cuda.current_stream().cuda_stream
-    p = rtow.params(W, H, spp, seed=args.seed, rank=rank, world=world)
+        self.args, self.rank, self.world = args, rank, world
+        torch.cuda.set_device(local)
+        self.device = torch.device("cuda", local)
+        W, H = args.width, args.height
+        self.scene = rtow.Scene.build(args.scene, n=max(args.n, 1), image="synthetic", scene_seed=1)
+        self.cam = rtow.camera_main(W, H)
+        self.ctx = rtow.Context(local)
+        self.ctx.upload(self.scene)
+        self.stride = rtow.rank_tile_count(W, H, 0, world) * 64  # rank 0 holds the most tiles
+        self.slab = torch.zeros(self.stride * 4, dtype=torch.uint8, device=self.device)
+        self.gathered = torch.zeros((world, self.stride * 4), dtype=torch.uint8, device=self.device) if rank == 0 else None
+        self.frame = torch.zeros((H, W, 4), dtype=torch.uint8, device=self.device) if rank == 0 else None
+        self.stream = torch.cuda.current_stream().cuda_stream
+        self.p = rtow.params(W, H, args.spp, seed=args.seed, rank=rank, world=world)
+        # load the code objects once (not a step: the warmup steps stay the contract's)
+        self.ctx.render_tiles_device(self.cam, rtow.params(W, H, 1, seed=args.seed, rank=rank, world=world),
+                                     self.slab.data_ptr(), None, self.stream)
+        torch.cuda.synchronize()
 
-    def step():
-        return frame_step(lambda sl: ctx.render_tiles_device(cam, p, sl.data_ptr(), None, stream),
-                          lambda g: ctx.assemble_device(W, H, world, g.data_ptr(), stride, frame.data_ptr(), stream),
-                          slab, gathered, rank, world, dist)
+    def init_kwargs(self):
+        return {"device_id": self.device}
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    segs, samples, kms = 0, 0, []
-    for _ in range(args.steps):
-        st = step()
-        segs += st.segments
-        samples += st.samples
-        kms.append(st.kernel_ms)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    tot = torch.tensor([float(segs), float(samples)], dtype=torch.float64, device="cuda")
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if distributed:
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    segs_all, samples_all, elapsed = float(tot[0]), float(tot[1]), float(el[0])
+    def step(self, dist):
+        W, H = self.args.width, self.args.height
+        return frame_step(
+            lambda sl: self.ctx.render_tiles_device(self.cam, self.p, sl.data_ptr(), None, self.stream),
+            lambda g: self.ctx.assemble_device(W, H, self.world, g.data_ptr(), self.stride, self.frame.data_ptr(),
+                                               self.stream),
+            self.slab, self.gathered, self.rank, self.world, dist)
 
-    if rank == 0:
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize()
+
+    def report(self, segs, steps, mean_kms):
+        """Rank 0's extra fields: cpu_baseline (N=1 only) and the roofline."""
+        import rtow
+
+        args, world = self.args, self.world
         threads, cpu_info = rtow.host_threads()
         if args.cpu_threads:
             threads = args.cpu_threads
         if args.no_cpu:
             base, bpr, counts = None, None, {}
         elif world == 1:
-            base, bpr, counts = cpu_baseline(scene, cam, args, threads)
+            base, bpr, counts = cpu_baseline(self.scene, self.cam, args, threads)
             base.update(cpu_info)
         else:  # the CPU baseline is quoted at N=1 only; bytes/ray from a smaller oracle sample
             args.cpu_pixels = max(1, args.cpu_pixels // 10)
             args.cpu_kind = "port"
-            _, bpr, counts = cpu_baseline(scene, cam, args, threads)
+            _, bpr, counts = cpu_baseline(self.scene, self.cam, args, threads)
             base = None
-        mean_kms = float(np.mean(kms))
-        launch_rays = segs / max(args.steps, 1)
-        roof = roofline(args, world, launch_rays, mean_kms, bpr, rtow.source_hash())
+        launch_rays = segs / max(steps, 1)
+        return {"roofline": roofline(args, world, launch_rays, mean_kms, bpr, rtow.source_hash()),
+                "cpu_baseline": base,
+                "oracle_counts": {k: round(v, 3) for k, v in counts.items()}}
+
+    def close(self):
+        self.ctx.close()
+
+
+def run(args, make_rank):
+    """The timed loop of every rank: W warmup steps, then exactly K steps
+    between barrier + device synchronize on both sides; the whole-job rate is
+    all ranks' rays over the slowest rank's time.  Rank 0 prints the line."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    R = make_rank(args, rank, world, local)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group(R.backend, **R.init_kwargs())
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        R.step(dist)
+    barrier()
+    R.sync()
+    t0 = time.perf_counter()
+    segs, samples, kms = 0, 0, []
+    for _ in range(args.steps):
+        st = R.step(dist)
+        segs += st.segments
+        samples += st.samples
+        kms.append(st.kernel_ms)
+    R.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    mean_kms = float(np.mean(kms)) if kms else 0.0
+    tot = torch.tensor([float(segs), float(samples)], dtype=torch.float64, device=R.device)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=R.device)
+    rk = torch.tensor([mean_kms], dtype=torch.float64, device=R.device)
+    rank_kms = [rk.clone() for _ in range(world)]
+    if distributed:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_gather(rank_kms, rk)
+    segs_all, samples_all, elapsed = float(tot[0]), float(tot[1]), float(el[0])
+    per_rank = [round(float(t[0]), 2) for t in rank_kms]
+
+    if rank == 0:
+        scene, _, W0, H0, spp0, label = WORKLOADS[args.workload]
+        W, H, spp = args.width, args.height, args.spp
+        is_baseline_cfg = args.workload == "random_ned" and (W, H, spp, args.n) == (W0, H0, spp0, 487)
+        metric = BASELINE_METRIC if args.workload == "random_ned" else f"Mray/s + Msample/s, {label} {W0}×{H0}×{spp0}spp"
         out = {
-            "metric": "Mray/s + Msample/s, random_scene 1920×1080×1024spp at 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(segs_all / elapsed / 1e6, 2),
             "unit": "Mray/s",
             "msample_per_s": round(samples_all / elapsed / 1e6, 3),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 2),
+            "ms_per_step": round(elapsed * 1e3 / max(args.steps, 1), 2),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"randomScene_NED n={args.n} ({args.n + 1} hitables under one BvhNode), "
-                                   f"{W}x{H}x{spp}spp, depth 50, synthetic 2048x1024 earth texture",
-                       "width": W, "height": H, "spp": spp, "n": args.n, "scene_seed": 1, "render_seed": args.seed,
-                       "parallelism": f"tiles8x8 interleaved over {world} rank(s) + RCCL gather to rank 0"},
+            "config": {"workload": (f"randomScene_NED n={args.n} ({args.n + 1} hitables under one BvhNode), "
+                                    if scene == "random_ned" else f"{label} ({scene}), ")
+                                   + f"{W}x{H}x{spp}spp, depth 50, synthetic 2048x1024 earth texture",
+                       "scene": scene, "width": W, "height": H, "spp": spp, "n": args.n, "scene_seed": 1,
+                       "render_seed": args.seed, "baseline_config": is_baseline_cfg,
+                       "parallelism": f"tiles8x8 interleaved over {world} rank(s) + gather to rank 0"},
             "rays_per_sample": round(segs_all / max(samples_all, 1), 4),
             "rays_per_step": int(segs_all / max(args.steps, 1)),
-            "roofline": roof,
-            "cpu_baseline": base,
-            "oracle_counts": {k: round(v, 3) for k, v in counts.items()},
+            "rank_kernel_ms": {"min": min(per_rank), "max": max(per_rank), "per_rank": per_rank},
         }
+        out.update(R.report(segs, args.steps, mean_kms))
         print(json.dumps(out), flush=True)
-    ctx.close()
+    R.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def main(make_rank=HipRank, argv=None):
+    args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # N ranks were asked for and none were launched: start them (one
+        # process per GPU) instead of running one rank and reporting it
+        sys.exit(launch(args.gpus, sys.argv[1:] if argv is None else argv, script=sys.argv[0]))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    run(args, make_rank)
 
 
 if __name__ == "__main__":

@@ -334,7 +334,7 @@ int rtow_render(rtow_context* ctx, const rtow_camera* cam, const rtow_params* p,
  * the context's running sums and writes the average of everything so far.
  * The sums restart when `reset` is set, a scene is uploaded, or the camera
  * or any parameter other than spp / samples_per_chunk / blocks_per_cu /
- * flags changed.  total_spp
+ * RTOW_FLAG_STATS changed (RTOW_FLAG_CAMERA_DOF restarts them).  total_spp
  * (may be NULL) receives the samples per pixel accumulated.  F frames of S
  * spp, each one chunk (samples_per_chunk = S, or automatic chunking with
  * S <= 16), give the frame of one rtow_render of F*S spp with

@@ -24,6 +24,7 @@
 //   ref_harness camera_oriented <W> <H> <lookfrom xyz> <view xyz> <east xyz> <down xyz> <out.cam>
 //   ref_harness render <scene> <W> <H> <spp> <out_prefix> [opts]
 //   ref_harness bench  <scene> <W> <H> <spp> <pixels.u32> [opts]   (timing, JSON line)
+//       --racy: render with the reference's own shared std::mt19937_64 (see g_racy)
 //       writes <out_prefix>.lin (W*H*3 float32, framebuffer order) and
 //       <out_prefix>.bgra (W*H*4 bytes, main.cpp:982-989)
 // scenes: three_sphere | random_ned | cornell | cornell_smoke | final_ned
@@ -61,6 +62,14 @@ static uint64_t harness_env_scene_key() {
     return rtow_scene_key(seed);
 }
 
+// `bench --racy`: the reference as written (rngs.h:9-11, main.cpp:942-943):
+// every render thread draws from ONE std::mt19937_64, unsynchronised (a data
+// race, as in the reference).  The real engine type is named before the
+// #define below turns `mt19937_64` into the counter engine.
+using RealMt64 = std::mt19937_64;
+static RealMt64 g_shared_mt(5489u);
+static bool g_racy = false;
+
 struct CbEngine {
     using result_type = uint64_t;
     static constexpr uint64_t min() { return 0; }
@@ -70,6 +79,7 @@ struct CbEngine {
     static thread_local uint64_t total;
     uint64_t operator()() {
         ++total;
+        if (g_racy) return g_shared_mt();
         return (uint64_t)rtow_draw24(key, ctr++) << 40;
     }
     void seed(uint64_t) {}
@@ -295,6 +305,7 @@ struct Opts {
     int n = 100;
     uint64_t seed = 1;
     int threads = 0;
+    bool racy = false;
     std::string cwd;
 };
 
@@ -455,6 +466,7 @@ static Opts parseOpts(int argc, char** argv, int first) {
         else if (a == "--seed") o.seed = std::strtoull(next(), nullptr, 0);
         else if (a == "--threads") o.threads = std::atoi(next());
         else if (a == "--cwd") o.cwd = next();
+        else if (a == "--racy") o.racy = true;
         else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); std::exit(2); }
     }
     return o;
@@ -562,6 +574,7 @@ int main(int argc, char** argv) {
         Camera* cam = mainCamera(W, H);
         int nt = o.threads > 0 ? o.threads : (int)std::thread::hardware_concurrency();
         std::vector<double> sums((size_t)nt, 0.0);
+        g_racy = o.racy;  // the scene is built; the render draws from the shared engine
         std::vector<std::thread> ts;
         auto t0 = std::chrono::steady_clock::now();
         for (int t = 0; t < nt; t++)
@@ -570,8 +583,9 @@ int main(int argc, char** argv) {
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         double sum = 0.0;
         for (double x : sums) sum += x;
-        std::printf("{\"seconds\": %.6f, \"pixels\": %zu, \"samples\": %llu, \"threads\": %d, \"checksum\": %.9g}\n",
-                    sec, pix.size(), (unsigned long long)pix.size() * spp, nt, sum);
+        std::printf("{\"seconds\": %.6f, \"pixels\": %zu, \"samples\": %llu, \"threads\": %d, \"checksum\": %.9g, "
+                    "\"racy\": %s}\n",
+                    sec, pix.size(), (unsigned long long)pix.size() * spp, nt, sum, o.racy ? "true" : "false");
         return 0;
     }
 #ifdef RTOW_HARNESS_DROPIN

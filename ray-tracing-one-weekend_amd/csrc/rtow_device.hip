@@ -2936,12 +2936,13 @@ struct Bounds {
             r = c;
             break;
         }
-        case DK_PROG:  // a medium is asked in place; any other item below a continuation (2 entries)
+        case DK_PROG:  // every item (media too) runs below a two-entry continuation
             for (uint32_t p = idx; p < L.prog.size() && L.prog[p].op != PROG_END; p++) {
                 if (L.prog[p].op != PROG_ITEM) continue;
                 const uint32_t it = L.prog[p].arg;
                 auto c = need(it, inMedium);
-                const uint32_t cont = (it >> KIND_SHIFT) == DK_MEDIUM ? 0u : 2u;
+                // the kernel pushes (tin, DK_PROGNEXT) for every item, media included
+                const uint32_t cont = 2u;
                 r = {std::max(r.first, cont + c.first), std::max(r.second, c.second)};
             }
             break;
@@ -3900,12 +3901,14 @@ namespace {
 int progressiveCore(rtow_context* c, const rtow_camera* cam, const rtow_params& q, int reset, uint8_t* slab_bgra,
                     float* slab_lin, uint8_t* fb_bgra, float* fb_lin, hipStream_t st, uint32_t* total_spp,
                     rtow_stats* stats) {
-    // what the accumulated samples were rendered with: camera + every param but spp / chunking
+    // what the accumulated samples were rendered with: camera + every param but
+    // spp / chunking / the statistics flag (RTOW_FLAG_CAMERA_DOF changes the
+    // image, so it is part of the key)
     rtow_params key = q;
     key.spp = 0;
     key.samples_per_chunk = 0;
     key.blocks_per_cu = 0;
-    key.flags = 0;
+    key.flags = q.flags & ~(uint32_t)RTOW_FLAG_STATS;
     std::vector<uint8_t> sig(sizeof(rtow_camera) + sizeof(rtow_params));
     std::memcpy(sig.data(), cam, sizeof(rtow_camera));
     std::memcpy(sig.data() + sizeof(rtow_camera), &key, sizeof(rtow_params));

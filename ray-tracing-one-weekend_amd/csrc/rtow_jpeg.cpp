@@ -1,6 +1,20 @@
 // rtow_jpeg.cpp -- the JPEG reader on the texture path: what stbi_load() (the
 // reference's stb_image.h v2.22, scenes.h:140) returns for a JPEG, restated.
 //
+// stb_image (https://github.com/nothings/stb, the reference vendors v2.22 as
+// stb_image.h) is by Sean Barrett and contributors, dual-licensed: public
+// domain (unlicense.org) or MIT.  MIT notice for the restated parts:
+//   Copyright (c) 2017 Sean Barrett.  Permission is hereby granted, free of
+//   charge, to any person obtaining a copy of this software and associated
+//   documentation files (the "Software"), to deal in the Software without
+//   restriction, including without limitation the rights to use, copy, modify,
+//   merge, publish, distribute, sublicense, and/or sell copies of the
+//   Software, and to permit persons to whom the Software is furnished to do
+//   so, subject to the following conditions: The above copyright notice and
+//   this permission notice shall be included in all copies or substantial
+//   portions of the Software.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT
+//   WARRANTY OF ANY KIND, EXPRESS OR IMPLIED.
+//
 // scenes.h:140 loads ./input_images/1_earth_8k.jpg with stbi_load(path, &nx,
 // &ny, &nn, 0) and hands the pixels to ImageTexture.  rtow_image_decode_jpeg
 // produces the same bytes: baseline and progressive Huffman JPEG, 8-bit,
@@ -479,6 +493,14 @@ struct Decoder {
         for (int i = 0; i < img_n; ++i) {
             h_max = std::max(h_max, comp[i].h);
             v_max = std::max(v_max, comp[i].v);
+        }
+        // sampling factors that do not divide the maximum (H=3 beside H=2)
+        // would make the colour conversion read a row past a component plane
+        // (stb 2.22 accepts them; later stb versions reject them the same way,
+        // and 2.22's output for such files is undefined)
+        for (int i = 0; i < img_n; ++i) {
+            if (h_max % comp[i].h != 0) return fail("bad H");
+            if (v_max % comp[i].v != 0) return fail("bad V");
         }
         mcu_x = (img_x + h_max * 8 - 1) / (h_max * 8);
         mcu_y = (img_y + v_max * 8 - 1) / (v_max * 8);

@@ -224,7 +224,16 @@ def rms(a, b):
 
 
 # ---- editing flattened scenes (tie / edge-case tests) ----------------------
-HIT_SPHERE, HIT_MOVING_SPHERE, HIT_TRANSLATE, HIT_BVH_NODE = 1, 2, 7, 11
+HIT_SPHERE, HIT_MOVING_SPHERE, HIT_TRANSLATE, HIT_LIST, HIT_BVH_NODE = 1, 2, 7, 9, 11
+
+
+def scene_check(scene):
+    """rtow_scene_check on any object with a view_ptr: (stack_need, chain_need)."""
+    import rtow
+
+    sn, cn = ctypes.c_uint32(), ctypes.c_uint32()
+    rtow.check(rtow.lib().rtow_scene_check(scene.view_ptr, ctypes.byref(sn), ctypes.byref(cn)), "rtow_scene_check")
+    return sn.value, cn.value
 
 
 def scene_dict(scene):

@@ -3,8 +3,11 @@ step (bench.frame_step: render the rank's slab, one gather to rank 0, rank 0
 assembles): the C oracle stands in for the GPU kernel and rtow.assemble for
 assemble_kernel -- the partition, the gather and the assembly are what is
 under test.  The frame must equal the single-rank frame bit for bit."""
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -80,3 +83,39 @@ def test_partition_is_a_bijection(W, H, world):
     seen = np.concatenate([rtow.rank_pixels(W, H, r, world) for r in range(world)])
     seen = seen[seen >= 0]
     assert seen.size == W * H and np.array_equal(np.sort(seen), np.arange(W * H))
+
+
+def _stub_cmd(*extra):
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench_stub_worker.py")
+    return [sys.executable, worker, "--workload", "cornell_smoke", "--width", "29", "--height", "21", "--spp", "4",
+            "--steps", "2", "--warmup", "1", "--no-cpu", *extra]
+
+
+def test_bench_launcher_starts_the_ranks(tmp_path):
+    """`bench.py --gpus 2` run directly (no WORLD_SIZE): bench.main starts two
+    ranks itself (torch.distributed.run child) -- here with the oracle stub rank
+    of tests/bench_stub_worker.py, gloo on the CPU -- and the line reports both
+    ranks; the frame equals the single-rank oracle frame bit for bit."""
+    out = str(tmp_path / "frame.npy")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["RTOW_BENCH_STUB_OUT"] = out
+    r = subprocess.run(_stub_cmd("--gpus", "2"), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["steps"] == 2 and line["warmup"] == 1
+    assert len(line["rank_kernel_ms"]["per_rank"]) == 2
+    assert line["rank_kernel_ms"]["min"] <= line["rank_kernel_ms"]["max"]
+    W, H, spp = 29, 21, 4
+    scene = rtow.Scene.build("cornell_smoke")
+    cam = sio.RtowCamera.from_buffer_copy(bytes(rtow.camera_main(W, H)))
+    _, full, c = sio.oracle_render(scene.view_ptr, cam, sio.default_params(W, H, spp, seed=1))
+    assert line["rays_per_step"] == c.segments
+    assert np.array_equal(np.load(out).reshape(-1, 4), full.reshape(-1, 4))
+
+
+def test_bench_refuses_a_world_that_differs_from_gpus():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run(_stub_cmd("--gpus", "2"), env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr

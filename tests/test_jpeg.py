@@ -57,6 +57,22 @@ def test_corrupt_input_fails_loudly():
         rtow.decode_jpeg(data[:40])
 
 
+def test_sampling_factors_that_do_not_divide_fail_loudly():
+    """A SOF whose sampling factors do not divide the maximum (H=3 beside
+    H=2): the colour conversion would read past a component plane; rejected
+    as later stb versions reject it (stb 2.22's output is undefined there)."""
+    data = bytearray(open(os.path.join(JDIR, "yuv420_q75.jpg"), "rb").read())
+    k = next(i for i in range(len(data) - 1) if data[i] == 0xFF and data[i + 1] in (0xC0, 0xC2))
+    assert data[k + 9] == 3  # three components
+    data[k + 11] = 0x31  # component 0: H=3, V=1
+    data[k + 14] = 0x21  # component 1: H=2, V=1
+    with pytest.raises(rtow.RtowError, match="bad H"):
+        rtow.decode_jpeg(bytes(data))
+    data[k + 11], data[k + 14] = 0x13, 0x12  # the same for V
+    with pytest.raises(rtow.RtowError, match="bad V"):
+        rtow.decode_jpeg(bytes(data))
+
+
 @pytest.mark.skipif(not (os.path.isdir(REF_IMAGES) and os.access(HARNESS, os.X_OK)),
                     reason="needs /root/reference and oracle/_ref/ref_harness (build container)")
 def test_reference_input_images_bit_exact(tmp_path):

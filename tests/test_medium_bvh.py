@@ -75,3 +75,53 @@ def test_gpu_medium_bvh_matches_reference(gpu_ctx, tree):
     assert np.mean(bgra != gbgra) < 0.01
     _, _, cnt = sio.oracle_render(ctypes.addressof(arrays.view), ocam, op)
     assert st.segments == cnt.segments
+
+
+def _medium_list_boundary_world():
+    """BvhNode(ConstantMedium(boundary = HitableList[A, B]), Sphere S): the
+    medium's boundary needs the nested general traversal, below a BvhNode."""
+    d = sio.scene_dict(rtow.Scene.build("random_ned", n=4, image="none"))  # textures + Perlin tables
+    h = np.zeros(6, sio.HITABLE)
+    h[0]["kind"], h[0]["a"], h[0]["b"] = sio.HIT_BVH_NODE, 1, 2
+    h[0]["f"][:6] = [1, -3, -3, 4, 3, 3]  # the main camera sits at the origin looking along +x
+    h[1]["kind"], h[1]["a"], h[1]["b"] = 12, 3, 1  # RTOW_HIT_CONSTANT_MEDIUM: boundary, phase material
+    h[1]["f"][0] = 2.0
+    h[2]["kind"], h[2]["a"] = sio.HIT_SPHERE, 0
+    h[2]["f"][:4] = [2.5, 0, 1.0, 0.5]
+    h[3]["kind"], h[3]["a"], h[3]["b"] = sio.HIT_LIST, 0, 2
+    for k, c in ((4, -1.0), (5, 1.0)):
+        h[k]["kind"], h[k]["a"] = sio.HIT_SPHERE, 0
+        h[k]["f"][:4] = [2.5, c, 0, 0.8]
+    d["hitables"], d["root"] = h, 0
+    d["refs"] = np.array([4, 5], np.uint32)
+    m = np.zeros(2, sio.MATERIAL)
+    m[0]["kind"], m[0]["texture"] = 1, 0  # Lambertian
+    m[1]["kind"], m[1]["texture"] = 5, 0  # Isotropic
+    d["materials"] = m
+    return d
+
+
+def test_stack_need_counts_the_continuation_of_a_medium_item():
+    """Every DProg item -- a medium too -- runs below the two-entry
+    continuation (tin, DK_PROGNEXT) the kernel pushes, so the medium item
+    needs 2 + its boundary's 1 (the list's DK_LISTNEXT) = 3 entries."""
+    d = _medium_list_boundary_world()
+    world = sio.ArrayScene(d)
+    sn, _ = sio.scene_check(world)
+    assert sn == 3, sn
+
+
+@pytest.mark.gpu
+def test_gpu_medium_with_list_boundary_below_bvh(gpu_ctx):
+    d = _medium_list_boundary_world()
+    W, H, spp = 32, 24, 16
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, spp, seed=4)
+    world = sio.ArrayScene(d)  # keeps the arrays alive while their pointers are used
+    gpu_ctx.upload(world)
+    _, lin, st = gpu_ctx.render(cam, p)
+    olin, _, cnt = sio.oracle_render(world.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                     sio.RtowParams.from_buffer_copy(bytes(p)))
+    assert cnt.medium_calls > 0
+    assert st.segments == cnt.segments
+    assert (sio.rms(lin.reshape(-1, 3), olin) <= 1e-4).all()

@@ -55,6 +55,29 @@ def test_progressive_restarts_on_camera_change(gpu_ctx):
 
 
 @pytest.mark.gpu
+def test_progressive_restarts_when_dof_turns_on(gpu_ctx):
+    """RTOW_FLAG_CAMERA_DOF changes the image, so switching it restarts the
+    running sums (pinhole and depth-of-field samples are never averaged into
+    one frame); RTOW_FLAG_STATS does not."""
+    W, H = 40, 24
+    scene = rtow.Scene.build("three_sphere")
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, 4, seed=1)
+    gpu_ctx.render_progressive(cam, p, reset=True)
+    pd = rtow.params(W, H, 4, seed=1)
+    pd.flags |= rtow.FLAG_CAMERA_DOF
+    _, lin, total, _ = gpu_ctx.render_progressive(cam, pd)
+    assert total == 4
+    _, one, _ = gpu_ctx.render(cam, pd)
+    assert np.array_equal(lin, one)
+    ps = rtow.params(W, H, 4, seed=1)
+    ps.flags = pd.flags ^ rtow.FLAG_STATS
+    _, _, total, _ = gpu_ctx.render_progressive(cam, ps)
+    assert total == 8
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("scene", ["random_ned", "cornell"])
 def test_oriented_camera_render_matches_oracle(scene, gpu_ctx):
     c = CAMS[2]

@@ -14,6 +14,7 @@ import glob
 import json
 import os
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "ray-tracing-one-weekend_amd"))
@@ -28,7 +29,7 @@ def bench_line(log):
 
 
 def main(out):
-    summary = {"source_hash": rtow.source_hash()}
+    summary = {"source_hash": rtow.source_hash(), "created": int(time.time())}
     passes = {}
     for d in sorted(glob.glob(os.path.join(out, "p[0-9]*"))):
         if not os.path.isdir(d):
@@ -37,6 +38,7 @@ def main(out):
         b = bench_line(d + ".log")
         cfg = b["config"]
         config = [cfg["width"], cfg["height"], cfg["spp"], cfg["n"], b["n_gpus"]]
+        summary.setdefault("workload", cfg.get("scene", "random_ned"))
         if summary.setdefault("config", config) != config:
             raise SystemExit(f"{name}: config {config} differs from {summary['config']}")
         rays = b["rays_per_step"]
