@@ -22,6 +22,47 @@ sys.path[:0] = [os.path.join(HERE, "..", "tests"), os.path.join(HERE, "..", "ray
 import rtow  # noqa: E402
 import scene_io as sio  # noqa: E402
 
+sys.path.insert(0, os.path.join(HERE, ".."))
+import bench  # noqa: E402
+
+
+def pmc_roofline(scene, W, H, segments, kernel_ms, src_hash):
+    """The VALU-issue roofline of this config's trace kernel (bench.py's
+    definition): wave-instructions per ray from the newest PMC summary of the
+    same workload and frame size (profiles/*/pmc_summary.json, this build's
+    source hash preferred; its spp may be lower: VALU per ray does not depend
+    on it) x the rays of this launch / its kernel time."""
+    import glob
+
+    best = None
+    for f in glob.glob(os.path.join(HERE, "..", "profiles", "*", "pmc_summary.json")):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload", "random_ned") != scene or d.get("config", [0, 0])[:2] != [W, H]:
+            continue
+        if "SQ_INSTS_VALU" not in d:
+            continue
+        key = (d.get("source_hash") == src_hash, d.get("created", 0), os.path.getmtime(f))
+        if best is None or key > best[0]:
+            best = (key, f, d)
+    if best is None:
+        return None
+    _, f, d = best
+    vpr = d["SQ_INSTS_VALU"] / d["rays_per_launch"]
+    achieved = vpr * segments / (kernel_ms * 1e-3) / 1e9
+    lane = d["SQ_THREAD_CYCLES_VALU"] / (d["SQ_ACTIVE_INST_VALU"] * 64) if "SQ_THREAD_CYCLES_VALU" in d else None
+    out = {"bound": "valu", "achieved": round(achieved, 1), "peak": bench.VALU_PEAK_G, "unit": "Gwave-instr/s",
+           "frac": round(achieved / bench.VALU_PEAK_G, 4), "valu_per_ray": round(vpr, 3),
+           "lane_util": round(lane, 4) if lane is not None else None,
+           "useful_lane_frac": round(achieved / bench.VALU_PEAK_G * lane, 4) if lane is not None else None,
+           "pmc": os.path.relpath(f, os.path.join(HERE, "..")), "pmc_config": d.get("config"),
+           "pmc_matches_build": d.get("source_hash") == src_hash}
+    if "WRITE_SIZE" in d:
+        out["write_bytes_per_ray"] = round(d["WRITE_SIZE"] * 1024 / d["rays_per_launch"], 2)
+    return out
+
 CONFIGS = {
     1: ("three-sphere lambertian scene 200x100x8spp", "three_sphere", 0, 200, 100, 8, 1),
     2: ("book-1 random_scene (n=487) 1920x1080x1024spp", "random_ned", 487, 1920, 1080, 1024, 1),
@@ -78,6 +119,7 @@ def main():
                "segments": st.segments, "rays_per_sample": round(st.segments / max(st.samples, 1), 4),
                "seconds": round(wall, 3), "kernel_ms": round(st.kernel_ms, 2),
                "mray_per_s": round(st.segments / wall / 1e6, 2), "msample_per_s": round(st.samples / wall / 1e6, 3),
+               "roofline": pmc_roofline(name, W, H, st.segments, st.kernel_ms, rtow.source_hash()),
                "cpu_baseline": cpu_rate(scene, cam, W, H, spp, args.cpu_seconds, threads)}
         if world > 1:
             out["note"] = (f"one GPU rendered rank 0's 1/{world} share; {world} GPUs render the frame in about "

@@ -7,7 +7,7 @@
 # then tools/pmc_summarize.py writes pmc_summary.json: the trace kernel's
 # counters per launch, tagged with the build's source hash, the config and
 # the rays of that launch -- what bench.py's VALU roofline reads.
-#   bash tools/profile_bench.sh TAG [extra bench.py args]
+#   bash tools/profile_bench.sh TAG [extra bench.py args, e.g. --workload cornell]
 # Output: gpurun_out/prof_TAG/ (copy bench.json, kernel_stats.csv and
 # pmc_summary.json into profiles/TAG/).
 set -o pipefail
