@@ -43,17 +43,22 @@ def main(out):
             raise SystemExit(f"{name}: config {config} differs from {summary['config']}")
         rays = b["rays_per_step"]
         kms = b["roofline"]["kernel_ms"]
-        vals, kernel = {}, None
+        # per dispatch (bench.py's rank setup renders one 1-spp frame before
+        # the step: the step's launch is the trace_kernel dispatch with the
+        # largest counter values)
+        disp, kernel = {}, None
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 if "trace_kernel" not in r["Kernel_Name"]:
                     continue
-                vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                v = disp.setdefault(r.get("Dispatch_Id") or r.get("Correlation_Id"), {})
+                v[r["Counter_Name"]] = v.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
                 kernel = r["Kernel_Name"][:96]
                 summary["_vgpr"] = int(r.get("VGPR_Count") or r.get("Arch_VGPR_Count") or 0)
                 summary["_grid"] = int(r["Grid_Size"])
-        if not vals:
+        if not disp:
             raise SystemExit(f"{name}: no trace_kernel counters")
+        vals = max(disp.values(), key=lambda v: sum(v.values()))
         # counters per launch, normalised to the first pass's ray count (the
         # launches trace the same frame; ray counts agree to the last ray)
         rays0 = summary.setdefault("rays_per_launch", rays)
