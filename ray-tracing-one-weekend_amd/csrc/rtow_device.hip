@@ -1592,37 +1592,96 @@ __device__ __forceinline__ void shade_segment(const DevScene& S, const DevParams
 
 // ---------------------------------------------------------------------------
 // Pixel sums.  A work item's chunk sum (its samples added in order, in float,
-// as main.cpp:946 adds them) goes into the pixel's sum as an unsigned 32.32
-// fixed-point number: fx = trunc(sum * 2^32), added with 64-bit integer
-// atomics.  Integer addition is associative, so the pixel's sum is the same
-// whatever order the chunks finish in (no [chunk][pixel] buffer, 32 B per
-// pixel, the frame deterministic and independent of the rank split), and
-// progressive frames add into the same sums (any chunking gives the same
-// frame).  The truncation is below 2^-32 per chunk; a chunk sum must stay
-// below 2^24 per channel (every contribution is emitted radiance times a
-// throughput <= 1: the reference's scenes stay below 20 per sample), else
-// the render fails with RTOW_E_UNSUPPORTED (fx_range).  The pixel value is
-// then (float)(fx * 2^-32), averaged as vec3.h:133-139 does.
-constexpr float FX_CHUNK_LIMIT = 16777216.0f;  // 2^24
-__device__ __forceinline__ void fx_add(unsigned long long* dst, F3 acc, uint32_t& range) {
+// as main.cpp:946 adds them) goes into the pixel's sum as a signed 192-bit
+// fixed-point number with 32 fraction bits: q = trunc(sum * 2^32), three
+// 64-bit limbs per channel (limb k in plane k of the sums buffer), added with
+// 64-bit integer atomics and explicit carries (fx_add192).  Integer addition
+// is associative, so the pixel's sum is the same whatever order the chunks
+// finish in (no [chunk][pixel] buffer, the frame deterministic and
+// independent of the rank split), and progressive frames add into the same
+// sums (any chunking gives the same frame).  Every finite float fits: |sum| <
+// 2^128, so |q| < 2^160, and 2^32 chunks of those stay below 2^192 -- any
+// emitter the reference's float accumulation (main.cpp:939-955) accepts
+// renders, negative values included (two's complement).  The truncation is
+// below 2^-32 per chunk.  Only a NaN or infinite chunk sum fails the render
+// (RTOW_E_UNSUPPORTED, fx_range).  In the usual range (0 <= sum, pixel total
+// < 2^32) only limb 0 is ever touched: one atomic per channel.  The pixel
+// value is (float)(q * 2^-32), averaged as vec3.h:133-139 does.
+__device__ __forceinline__ void fx_limbs(float x, unsigned long long& l0, unsigned long long& l1,
+                                         unsigned long long& l2) {
+    const uint32_t b = __float_as_uint(x);
+    const uint32_t e = (b >> 23) & 255u;
+    const unsigned long long m = (b & 0x7fffffu) | (e ? 0x800000u : 0u);
+    // |x| * 2^32 = m * 2^sh, sh = max(e, 1) - 150 + 32
+    const int sh = (int)(e ? e : 1u) - 118;
+    l0 = l1 = l2 = 0;
+    if (sh < 0) {
+        l0 = sh > -24 ? m >> -sh : 0ull;  // truncation of the bits below 2^-32
+    } else {
+        const uint32_t w = (uint32_t)sh >> 6, r = (uint32_t)sh & 63u;
+        const unsigned long long lo = m << r, hi = r ? m >> (64u - r) : 0ull;
+        if (w == 0) {
+            l0 = lo;
+            l1 = hi;
+        } else if (w == 1) {
+            l1 = lo;
+            l2 = hi;
+        } else {
+            l2 = lo;
+        }
+    }
+    if (b >> 31) {  // two's complement of the 192-bit magnitude
+        l0 = ~l0 + 1ull;
+        l1 = ~l1 + (l0 == 0 ? 1ull : 0ull);
+        l2 = ~l2 + ((l0 == 0 && l1 == 0) ? 1ull : 0ull);
+    }
+}
+// (l2, l1, l0) added to the 192-bit sum at p, p + plane, p + 2 plane: each
+// limb's carry out is read from the atomic's old value, so the limbs hold the
+// exact sum of all adds (mod 2^192) whatever their order
+__device__ __forceinline__ void fx_add192(unsigned long long* p, size_t plane, unsigned long long l0,
+                                          unsigned long long l1, unsigned long long l2) {
+    unsigned long long c = 0;
+    if (l0) {
+        const unsigned long long o = atomicAdd(p, l0);
+        c = (o + l0 < o) ? 1ull : 0ull;
+    }
+    const unsigned long long t1 = l1 + c;
+    unsigned long long c2 = (t1 < l1) ? 1ull : 0ull;  // l1 = 2^64 - 1 plus a carry: wraps to 0, carries on
+    if (t1) {
+        const unsigned long long o = atomicAdd(p + plane, t1);
+        c2 |= (o + t1 < o) ? 1ull : 0ull;
+    }
+    const unsigned long long t2 = l2 + c2;
+    if (t2) atomicAdd(p + 2 * plane, t2);
+}
+__device__ __forceinline__ void fx_add(unsigned long long* dst, size_t plane, F3 acc, uint32_t& range) {
     const float v[3] = {acc.x, acc.y, acc.z};
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const float x = v[k];
-        if (!(x >= 0.0f && x < FX_CHUNK_LIMIT)) {  // also NaN
+        if (!(fabsf(x) <= FLT_MAX)) {  // NaN or infinite
             range = 1;
             continue;
         }
-        // trunc(x * 2^32) exactly: the integer part, then the fraction
-        // (x - floor(x) is exact below 2^24) scaled by 2^32 and truncated
-        const uint32_t hi = (uint32_t)x;
-        const uint32_t lo = (uint32_t)((x - (float)hi) * 4294967296.0f);
-        const unsigned long long q = ((unsigned long long)hi << 32) | lo;
-        if (q) atomicAdd(dst + k, q);
+        unsigned long long l0, l1, l2;
+        fx_limbs(x, l0, l1, l2);
+        fx_add192(dst + k, plane, l0, l1, l2);
     }
 }
 
-__device__ __forceinline__ float fx_value(unsigned long long q) { return (float)((double)q * 0x1p-32); }
+// the signed 192-bit sum as a double: the usual case (l1 = l2 = 0) is
+// exactly (double)l0 * 2^-32
+__device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long long l1, unsigned long long l2) {
+    const bool neg = (l2 >> 63) != 0;
+    if (neg) {
+        l0 = ~l0 + 1ull;
+        l1 = ~l1 + (l0 == 0 ? 1ull : 0ull);
+        l2 = ~l2 + ((l0 == 0 && l1 == 0) ? 1ull : 0ull);
+    }
+    const double v = (double)l2 * 0x1p96 + (double)l1 * 0x1p32 + (double)l0 * 0x1p-32;
+    return (float)(neg ? -v : v);
+}
 
 // MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
 // chain), 2 general scene, 3 general scene with media, 4 general scene with
@@ -1848,7 +1907,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             acc = add(acc, contrib);
             s++;
             if (s >= s_end) {
-                fx_add(fx + 4 * (size_t)lpx, acc, fx_range);
+                fx_add(fx + 4 * (size_t)lpx, 4 * (size_t)P.n_local_px, acc, fx_range);
                 need_item = true;
             } else {
                 need_sample = true;
@@ -1892,7 +1951,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
 // fx: the pixel sums (fixed point, see fx_add) of all P.sample_base + P.spp
 // samples -- this frame's chunks added by trace_kernel into the running sums
 // of the earlier progressive frames (sample_base 0: a fresh, zeroed buffer).
-#ifndef RTOW_TU_SIMPLE
+#if !defined(RTOW_TU_SIMPLE) && !defined(RTOW_TU_KERNELS)
 __global__ void resolve_kernel(DevParams P, const unsigned long long* fx, uint8_t* slab_bgra, float* slab_lin,
                                uint8_t* fb_bgra, float* fb_lin, unsigned long long* counters) {
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1909,8 +1968,9 @@ __global__ void resolve_kernel(DevParams P, const unsigned long long* fx, uint8_
         return;
     }
     const unsigned long long* sum = fx + 4 * (size_t)lp;
-    if ((sum[0] | sum[1] | sum[2]) >> 63) atomicAdd(&counters[13], 1ull);  // beyond 2^31 per channel
-    const F3 acc = f3(fx_value(sum[0]), fx_value(sum[1]), fx_value(sum[2]));
+    const size_t plane = 4 * (size_t)P.n_local_px;
+    const F3 acc = f3(fx_value(sum[0], sum[plane], sum[2 * plane]), fx_value(sum[1], sum[plane + 1], sum[2 * plane + 1]),
+                      fx_value(sum[2], sum[plane + 2], sum[2 * plane + 2]));
     const float k = (float)(1.0 / (double)(float)(P.sample_base + P.spp));  // vec3.h:133-139
     const F3 lin = f3(acc.x * k, acc.y * k, acc.z * k);
     const float sq[3] = {sqrtf(lin.x), sqrtf(lin.y), sqrtf(lin.z)};
@@ -1947,22 +2007,54 @@ __global__ void assemble_kernel(uint32_t W, uint32_t H, uint32_t world, uint32_t
     fb[i] = slabs[(size_t)rank * stride_px + slot * 64u + (y & 7u) * 8u + (x & 7u)];
 }
 
-#endif  // RTOW_TU_SIMPLE
+#endif  // host translation unit
 
-// The simple-scene kernel the bench runs (random scene, BVH in LDS) is
-// compiled in its own translation unit with -amdgpu-sched-strategy=
-// iterative-ilp (+2.8 % there, but -3..-6 % on the general kernels).
-#define RTOW_SIMPLE_HOT_ARGS DevScene, DevCam, DevParams, uint32_t*, unsigned long long*, unsigned long long*
-#ifdef RTOW_TU_SIMPLE
-template __global__ void trace_kernel<0, 16, 4, false, 512, true, false>(RTOW_SIMPLE_HOT_ARGS);
+// Every trace_kernel instantiation the host launches (launchWaves), listed
+// once: X(MODE, STACK, WAVES, PROF, BS, LDSN, DBG).  The host translation unit
+// declares them extern; the kernel translation units (-DRTOW_TU_KERNELS=m,
+// one per MODE, see the Makefile) instantiate them, so the modes compile in
+// parallel.  The simple-scene kernel the bench runs (random scene, BVH in LDS)
+// is compiled in its own unit with -amdgpu-sched-strategy=iterative-ilp
+// (RTOW_TU_SIMPLE: +2.8 % there, but -3..-6 % on the general kernels).
+#define RTOW_KERNEL_ARGS DevScene, DevCam, DevParams, uint32_t*, unsigned long long*, unsigned long long*
+#define RTOW_K_COMMON(X, M, S)                                                                    \
+    X(M, S, 1, false, BLOCK, false, true)                                                         \
+    X(M, S, 4, false, BLOCK, false, false)                                                        \
+    X(M, S, 3, false, BLOCK, false, false)                                                        \
+    X(M, S, 1, false, BLOCK, false, false)
+#define RTOW_K_PROF(X, M, S) X(M, S, 4, true, BLOCK, false, false)
+#define RTOW_K_DEEP(X, M) X(M, 64, 1, false, BLOCK, false, true) X(M, 64, 1, false, BLOCK, false, false)
+#define RTOW_KLIST_0(X) RTOW_K_COMMON(X, 0, 16) RTOW_K_PROF(X, 0, 16) RTOW_K_COMMON(X, 0, 32) RTOW_K_DEEP(X, 0)
+#define RTOW_KLIST_G(X, M)                                                                         \
+    RTOW_K_COMMON(X, M, 16) RTOW_K_PROF(X, M, 16) RTOW_K_COMMON(X, M, 20) RTOW_K_PROF(X, M, 20)   \
+    RTOW_K_COMMON(X, M, 32) RTOW_K_PROF(X, M, 32) RTOW_K_DEEP(X, M)
+#define RTOW_K_HOT(X) X(0, 16, 4, false, 512, true, false)
+#if defined(RTOW_TU_SIMPLE)
+#define RTOW_KX(M, S, W, P, B, L, D) template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
+RTOW_K_HOT(RTOW_KX)
+#elif defined(RTOW_TU_KERNELS)
+#define RTOW_KX(M, S, W, P, B, L, D) template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
+#if RTOW_TU_KERNELS == 0
+RTOW_KLIST_0(RTOW_KX)
 #else
-extern template __global__ void trace_kernel<0, 16, 4, false, 512, true, false>(RTOW_SIMPLE_HOT_ARGS);
+RTOW_KLIST_G(RTOW_KX, RTOW_TU_KERNELS)
 #endif
+#else
+#define RTOW_KX(M, S, W, P, B, L, D) \
+    extern template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
+RTOW_K_HOT(RTOW_KX)
+RTOW_KLIST_0(RTOW_KX)
+RTOW_KLIST_G(RTOW_KX, 2)
+RTOW_KLIST_G(RTOW_KX, 3)
+RTOW_KLIST_G(RTOW_KX, 4)
+RTOW_KLIST_G(RTOW_KX, 5)
+#endif
+#undef RTOW_KX
 
 }  // namespace rtow_k
 using namespace rtow_k;
 
-#ifndef RTOW_TU_SIMPLE
+#if !defined(RTOW_TU_SIMPLE) && !defined(RTOW_TU_KERNELS)
 
 // ===========================================================================
 // host side: scene conversion, context, C-ABI
@@ -3430,7 +3522,7 @@ struct rtow_context {
     bool has_scene = false;
     // work buffers
     void* d_work = nullptr;  // [0] work counter (u32) | [8..] u64 counters
-    unsigned long long* d_fx = nullptr;  // pixel sums of one render (fx_add), 32 B per local pixel
+    unsigned long long* d_fx = nullptr;  // pixel sums of one render (fx_add): three limb planes, 96 B per local pixel
     size_t fx_bytes = 0;
     uint8_t* d_fb = nullptr;  // rtow_render: BGRA frame + linear frame
     size_t fb_bytes = 0;
@@ -3510,10 +3602,6 @@ int launchWaves(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
         }
         if (c->waves == 4) return launchTrace<MODE, STACK, 4>(c, cam, P, bpc, st);
         if (c->waves == 3) return launchTrace<MODE, STACK, 3>(c, cam, P, bpc, st);
-        if constexpr (MODE == 0 || MODE == 2 || MODE == 3) {
-            if (c->waves == 5) return launchTrace<MODE, STACK, 5>(c, cam, P, bpc, st);
-            if (c->waves == 2) return launchTrace<MODE, STACK, 2>(c, cam, P, bpc, st);
-        }
     }
     return launchTrace<MODE, STACK, 1>(c, cam, P, bpc, st);
 }
@@ -3616,7 +3704,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
     if (rc) return rc;
     P.sample_base = sample_base;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t fx_need = (size_t)P.n_local_px * 4 * sizeof(unsigned long long);
+    const size_t fx_need = (size_t)P.n_local_px * 3 * 4 * sizeof(unsigned long long);  // three limb planes
     if (accum) {  // progressive: the running sums (zeroed by the caller when they restart)
         c->fx_cur = accum;
     } else {
@@ -3680,8 +3768,7 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
     }
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
     if (host_ctr[13])
-        return set_error(RTOW_E_UNSUPPORTED, "pixel sum out of the fixed-point range (a chunk of samples summed to "
-                                             ">= 2^24 or NaN, or a pixel to >= 2^31)");
+        return set_error(RTOW_E_UNSUPPORTED, "a chunk of samples summed to NaN or infinity");
     if (stats) {
         float k = 0, r = 0;
         HIP_TRY(hipEventElapsedTime(&k, c->ev[0], c->ev[1]));
@@ -3920,8 +4007,8 @@ int progressiveCore(rtow_context* c, const rtow_camera* cam, const rtow_params& 
     const uint32_t world = q.world ? q.world : 1;
     if (q.rank >= world) return set_error(RTOW_E_INVALID, "rank >= world");
     HIP_TRY(hipSetDevice(c->device));
-    const size_t acc_need = (size_t)rtow_rank_tile_count(q.width, q.height, q.rank, world) * 64 * 4 *
-                            sizeof(unsigned long long);
+    const size_t acc_need = (size_t)rtow_rank_tile_count(q.width, q.height, q.rank, world) * 64 * 3 * 4 *
+                            sizeof(unsigned long long);  // three limb planes (fx_add)
     if (c->accum_bytes < acc_need) c->accum_spp = 0;
     int rc = ensure((void**)&c->d_accum, &c->accum_bytes, acc_need);
     if (rc) return rc;
@@ -4024,4 +4111,4 @@ int rtow_assemble_device(rtow_context* c, uint32_t width, uint32_t height, uint3
 }
 
 }  // extern "C"
-#endif  // RTOW_TU_SIMPLE
+#endif  // host translation unit

@@ -338,3 +338,39 @@ def tie_scene(n=100):
     pos = {k: leaves.index(k) for k in (x, y)}
     early, late = sorted((x, y), key=lambda k: pos[k])
     return d, early, late
+
+
+# ---- scene-graph edits (tests build reference-legal worlds the fixtures do not hold)
+def copy_scene(d):
+    return {k: (v.copy() if hasattr(v, "copy") else v) for k, v in d.items()}
+
+
+def with_items(d, lst, items):
+    """A copy of d whose list hitable `lst` holds `items` (appended refs)."""
+    e = copy_scene(d)
+    e["hitables"][lst]["a"] = len(e["refs"])
+    e["hitables"][lst]["b"] = len(items)
+    e["refs"] = np.concatenate([e["refs"], np.array(items, np.uint32)])
+    return e
+
+
+def add_list(d, members):
+    """Append a HitableList hitable over `members`; returns (dict, its index)."""
+    e = copy_scene(d)
+    h = np.zeros(1, dtype=HITABLE)
+    h[0]["kind"] = HIT_LIST
+    h[0]["a"] = len(e["refs"])
+    h[0]["b"] = len(members)
+    e["refs"] = np.concatenate([e["refs"], np.array(members, np.uint32)])
+    e["hitables"] = np.concatenate([e["hitables"], h])
+    return e, len(e["hitables"]) - 1
+
+
+def bvh_leaves(h, i):
+    """The leaves of BvhNode i in left-to-right order (an n == 1 node once)."""
+    if h[i]["kind"] == HIT_BVH_NODE:
+        out = bvh_leaves(h, h[i]["a"])
+        if h[i]["b"] != h[i]["a"]:
+            out += bvh_leaves(h, h[i]["b"])
+        return out
+    return [int(i)]

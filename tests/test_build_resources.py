@@ -58,3 +58,12 @@ def test_default_kernels_scratch_bounded(kernels):
         assert k["scratch"] <= SCRATCH_BOUND[p["MODE"]], (p, k["scratch"])
         assert k["vgpr"] <= 128, p
     assert seen == {0, 2, 3, 4, 5}
+
+
+def test_each_kernel_compiled_once(kernels):
+    """The trace kernels come from their per-MODE translation units only (the
+    host unit declares them extern): no instantiation is compiled twice."""
+    names = [k["name"] for k in kernels]
+    assert len(names) == len(set(names))
+    modes = {codeobj.demangled_params(n)["MODE"] for n in names if codeobj.demangled_params(n)}
+    assert modes == {0, 2, 3, 4, 5}

@@ -205,10 +205,6 @@ def test_long_flat_list_matches_oracle(gpu_ctx):
     """A HitableList of 400 Boxes (final_ned's ground without its BvhNode) and
     of all random_ned spheres: lists are walked with one continuation entry on
     the stack, so their length is not bounded by the stack."""
-    import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
-    import isolate_ground as ig
-
     W, H, spp = 40, 24, 4
     cam = rtow.camera_main(W, H)
     p = rtow.params(W, H, spp, seed=6)
@@ -218,10 +214,10 @@ def test_long_flat_list_matches_oracle(gpu_ctx):
         inner = int(h[d["root"]]["a"])  # root Translate -> list (final) / BvhNode (random)
         if h[inner]["kind"] == 9:
             bvh = int(d["refs"][int(h[inner]["a"])])
-            e, L = ig.add_list(d, ig.leaves(h, bvh))
-            e = ig.with_items(e, inner, [L])
+            e, L = sio.add_list(d, sio.bvh_leaves(h, bvh))
+            e = sio.with_items(e, inner, [L])
         else:
-            e, L = ig.add_list(d, ig.leaves(h, inner))
+            e, L = sio.add_list(d, sio.bvh_leaves(h, inner))
             e["hitables"][e["root"]]["a"] = L
         sc = sio.ArrayScene(e)
         gpu_ctx.upload(sc)

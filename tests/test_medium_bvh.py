@@ -124,4 +124,4 @@ def test_gpu_medium_with_list_boundary_below_bvh(gpu_ctx):
                                      sio.RtowParams.from_buffer_copy(bytes(p)))
     assert cnt.medium_calls > 0
     assert st.segments == cnt.segments
-    assert (sio.rms(lin.reshape(-1, 3), olin) <= 1e-4).all()
+    assert sio.rms(lin.reshape(-1, 3), olin) <= 1e-4
