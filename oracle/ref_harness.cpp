@@ -228,6 +228,56 @@ static Hitable* mediumBvhNed() {
     return new HitableList(list, 3);
 }
 
+// Media the reference composes freely (constantMedium.h:26-31: the boundary is
+// any Hitable; hitableList.h:24-34: a list hands each item its closest hit so
+// far): a medium whose boundary is another medium, or a list holding one; and
+// media below a BvhNode behind an instance or inside a list.
+static Hitable* mediumNestedNed() {
+    Texture* white = new ConstantTexture(vec3(0.9, 0.9, 0.9));
+    Texture* teal = new ConstantTexture(vec3(0.2, 0.8, 0.7));
+    Texture* rose = new ConstantTexture(vec3(0.9, 0.4, 0.5));
+    Material* glass = new Dielectric(1.5);
+    Hitable** list = new Hitable*[6];
+    list[0] = new Sphere(vec3(10, 0, 101), 100, new Lambertian(new ConstantTexture(vec3(0.8, 0.8, 0.0))));
+    // a medium whose boundary is a medium
+    list[1] = new ConstantMedium(new ConstantMedium(new Sphere(vec3(10, -1.5, 0), 1.2, glass), 0.7f, white), 0.9f, teal);
+    // a medium whose boundary is a list holding a sphere and a medium over a Box
+    Hitable** inner = new Hitable*[2];
+    inner[0] = new Sphere(vec3(10, 1.6, 0.2), 0.8, glass);
+    inner[1] = new ConstantMedium(new Box(vec3(9.2, 1.2, -1.4), vec3(10.4, 2.8, -0.4), new Lambertian(white)), 1.5f, rose);
+    list[2] = new ConstantMedium(new HitableList(inner, 2), 0.6f, white);
+    list[3] = new Sphere(vec3(11, 0.2, -1.8), 0.6, new Metal(vec3(0.8, 0.8, 0.9), 0.1));
+    list[4] = new Sphere(vec3(7, 0.5, -4), 0.6, new DiffuseLight(new ConstantTexture(vec3(4, 4, 4))));
+    list[5] = new Sphere(vec3(12, -3, -1), 0.9, new Lambertian(new ConstantTexture(vec3(0.1, 0.2, 0.5))));
+    return new HitableList(list, 6);
+}
+
+static Hitable* mediumBvhWrappedNed() {
+    Texture* white = new ConstantTexture(vec3(0.9, 0.9, 0.9));
+    Texture* teal = new ConstantTexture(vec3(0.2, 0.8, 0.7));
+    Material* glass = new Dielectric(1.5);
+    Hitable** items = new Hitable*[5];
+    items[0] = new Sphere(vec3(10, 0, 0), 1, new Lambertian(new ConstantTexture(vec3(0.1, 0.2, 0.5))));
+    // behind a Translate
+    items[1] = new Translate(new ConstantMedium(new Sphere(vec3(0, 0, 0), 1, glass), 0.8f, white), vec3(10, -2.2, 0));
+    // inside a list: handed the list's closest hit so far (hitableList.h:24-34)
+    Hitable** l2 = new Hitable*[3];
+    l2[0] = new Sphere(vec3(9.4, 2.0, 0.3), 0.5, new Metal(vec3(0.8, 0.8, 0.9), 0.1));
+    l2[1] = new ConstantMedium(new Box(vec3(8, 1.5, -1), vec3(9.5, 3, 1), new Lambertian(white)), 0.5f, teal);
+    l2[2] = new Sphere(vec3(10.5, 2.6, -0.8), 0.4, new Lambertian(new ConstantTexture(vec3(0.7, 0.3, 0.2))));
+    items[2] = new HitableList(l2, 3);
+    // behind a RotateY over a Translate
+    items[3] = new RotateY(new Translate(new ConstantMedium(new Box(vec3(-0.6, -0.6, -0.6), vec3(0.6, 0.6, 0.6),
+                                                                     new Lambertian(white)), 1.2f, teal),
+                                         vec3(10.5, 0.8, -2.2)), 8);
+    items[4] = new ConstantMedium(new Sphere(vec3(12, 0, -2.5), 1.2, glass), 0.3f, white);
+    Hitable** list = new Hitable*[3];
+    list[0] = new Sphere(vec3(10, 0, 101), 100, new Lambertian(new ConstantTexture(vec3(0.8, 0.8, 0.0))));
+    list[1] = new BvhNode(items, 5, 0.0f, 1.0f);
+    list[2] = new Sphere(vec3(7, 0.5, -4), 0.6, new DiffuseLight(new ConstantTexture(vec3(4, 4, 4))));
+    return new HitableList(list, 3);
+}
+
 // Config 4: cornellBox_NED() with the smoke box that scenes.h:461-470 keeps
 // commented out, inserted at the position that code occupies (after the
 // rotated box, before the sphere medium).
@@ -330,6 +380,8 @@ static Hitable* buildWorld(const std::string& name, const Opts& o) {
     if (name == "cornell_smoke") return new Translate(cornellSmokeNed(), vec3(800, 0, 0));
     if (name == "three_sphere") return threeSphereNed();
     if (name == "medium_bvh") return mediumBvhNed();
+    if (name == "medium_nested") return mediumNestedNed();
+    if (name == "medium_bvh_wrapped") return mediumBvhWrappedNed();
     if (name == "final_ned") {
         bool used;
         return new Translate(finalSceneNed(&used), vec3(600, -278, 278));

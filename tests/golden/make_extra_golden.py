@@ -6,7 +6,11 @@
   oracle/_ref/ref_harness_dof -- the same harness as make_golden.py's,
   compiled with CAMERA_DOF_EN 1 (camera.h:124-126);
 * medium_bvh: ConstantMedium below a BvhNode (ref_harness.cpp mediumBvhNed:
-  the reference's classes, media in the BVH, one in an n == 1 node).
+  the reference's classes, media in the BVH, one in an n == 1 node);
+* medium_nested: a medium whose boundary is a medium, and one whose boundary
+  is a list holding a medium (ref_harness.cpp mediumNestedNed);
+* medium_bvh_wrapped: media below a BvhNode behind a Translate, inside a list
+  and behind RotateY(Translate(...)) (ref_harness.cpp mediumBvhWrappedNed).
 
 Writes <case>.{scn,lin,bgra} (texels stripped, as make_golden.py), the
 cameras, and manifest_extra.json (`flags`: the rtow_params flags the case
@@ -36,6 +40,8 @@ CASES = [
     ("dof_three_sphere", HARNESS_DOF, FLAG_CAMERA_DOF, "three_sphere", 100, "none", 64, 36, 16, 3),
     ("dof_random100", HARNESS_DOF, FLAG_CAMERA_DOF, "random_ned", 100, "synthetic", 48, 27, 16, 5),
     ("medium_bvh", HARNESS, 0, "medium_bvh", 100, "none", 64, 36, 64, 9),
+    ("medium_nested", HARNESS, 0, "medium_nested", 100, "none", 64, 36, 64, 11),
+    ("medium_bvh_wrapped", HARNESS, 0, "medium_bvh_wrapped", 100, "none", 64, 36, 64, 13),
 ]
 SCENE_SEED = 1
 
