@@ -296,8 +296,9 @@ int rtow_context_destroy(rtow_context* ctx);
 /* Host-only check that the device path can render `scene` (the conversion
  * rtow_scene_upload performs, without a GPU).  stack_need / chain_need (may
  * be NULL) receive the traversal-stack entries and instance nesting a ray
- * needs.  Returns RTOW_E_UNSUPPORTED (reason in rtow_last_error) e.g. for a
- * ConstantMedium below a BvhNode. */
+ * needs (for a world the exact-order kernel renders: the deepest hit() call
+ * chain).  Returns RTOW_E_UNSUPPORTED (reason in rtow_last_error) e.g. for a
+ * graph whose hit() recursion is deeper than 48 calls. */
 int rtow_scene_check(const rtow_scene* scene, uint32_t* stack_need, uint32_t* chain_need);
 /* Convert the scene graph to the device layout and copy it to HBM. */
 int rtow_scene_upload(rtow_context* ctx, const rtow_scene* scene);

@@ -278,6 +278,34 @@ static Hitable* mediumBvhWrappedNed() {
     return new HitableList(list, 3);
 }
 
+// An exact tie between a list item and a BvhNode item entered exactly at the
+// tied t: the wall rectangle (item 0) and the near faces of two Boxes in a
+// BvhNode (item 1) share the plane x = 10.  A ray through the overlap hits the
+// wall at t*, then HitableList::hit asks the BvhNode with (tmin, t*)
+// (hitableList.h:24-34); AABB::hit sees its box entered at exactly t* and
+// returns `tmax <= tmin` (aabb.h:22-43), so the Boxes' faces -- which would
+// take t == t* (closed interval, xy_rect.h) -- are never tested: the wall keeps
+// the record.  A third Box sits in a BvhNode whose box starts before the
+// plane (a sphere in front of it): there the face is tested and takes the tie.
+static Hitable* tieBvhEntryNed() {
+    Material* red = new Lambertian(new ConstantTexture(vec3(0.8, 0.1, 0.1)));
+    Material* blue = new Lambertian(new ConstantTexture(vec3(0.1, 0.2, 0.8)));
+    Material* green = new Lambertian(new ConstantTexture(vec3(0.1, 0.8, 0.2)));
+    Hitable** boxes = new Hitable*[2];
+    boxes[0] = new Box(vec3(10, -2.5, -1.5), vec3(11, -0.5, 0.5), blue);
+    boxes[1] = new Box(vec3(10, 0.5, -1.5), vec3(11.5, 2.5, 0.5), blue);
+    Hitable** front = new Hitable*[2];
+    front[0] = new Box(vec3(10, -1.0, 0.8), vec3(11, 1.0, 2.0), green);
+    front[1] = new Sphere(vec3(8.5, 3.0, 1.5), 0.3, green);
+    Hitable** list = new Hitable*[5];
+    list[0] = new YZRectangle(-3, 3, -2, 2.5, 10, red);
+    list[1] = new BvhNode(boxes, 2, 0.0f, 1.0f);
+    list[2] = new BvhNode(front, 2, 0.0f, 1.0f);
+    list[3] = new Sphere(vec3(7, 0.5, -4), 0.6, new DiffuseLight(new ConstantTexture(vec3(4, 4, 4))));
+    list[4] = new Sphere(vec3(10, 0, 101.5), 100, new Lambertian(new ConstantTexture(vec3(0.8, 0.8, 0.0))));
+    return new HitableList(list, 5);
+}
+
 // Config 4: cornellBox_NED() with the smoke box that scenes.h:461-470 keeps
 // commented out, inserted at the position that code occupies (after the
 // rotated box, before the sphere medium).
@@ -381,6 +409,7 @@ static Hitable* buildWorld(const std::string& name, const Opts& o) {
     if (name == "three_sphere") return threeSphereNed();
     if (name == "medium_bvh") return mediumBvhNed();
     if (name == "medium_nested") return mediumNestedNed();
+    if (name == "tie_bvh_entry") return tieBvhEntryNed();
     if (name == "medium_bvh_wrapped") return mediumBvhWrappedNed();
     if (name == "final_ned") {
         bool used;

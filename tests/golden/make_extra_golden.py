@@ -10,7 +10,9 @@
 * medium_nested: a medium whose boundary is a medium, and one whose boundary
   is a list holding a medium (ref_harness.cpp mediumNestedNed);
 * medium_bvh_wrapped: media below a BvhNode behind a Translate, inside a list
-  and behind RotateY(Translate(...)) (ref_harness.cpp mediumBvhWrappedNed).
+  and behind RotateY(Translate(...)) (ref_harness.cpp mediumBvhWrappedNed);
+* tie_bvh_entry: a list item and a BvhNode item tied at a t where the
+  BvhNode's box is entered exactly (ref_harness.cpp tieBvhEntryNed).
 
 Writes <case>.{scn,lin,bgra} (texels stripped, as make_golden.py), the
 cameras, and manifest_extra.json (`flags`: the rtow_params flags the case
@@ -42,6 +44,7 @@ CASES = [
     ("medium_bvh", HARNESS, 0, "medium_bvh", 100, "none", 64, 36, 64, 9),
     ("medium_nested", HARNESS, 0, "medium_nested", 100, "none", 64, 36, 64, 11),
     ("medium_bvh_wrapped", HARNESS, 0, "medium_bvh_wrapped", 100, "none", 64, 36, 64, 13),
+    ("tie_bvh_entry", HARNESS, 0, "tie_bvh_entry", 100, "none", 64, 36, 16, 15),
 ]
 SCENE_SEED = 1
 

@@ -45,3 +45,30 @@ def test_oracle_matches_reference_bit_exact(name):
     assert np.array_equal(lin.reshape(H, W, 3).view(np.uint32), glin.view(np.uint32))
     assert np.array_equal(bgra.reshape(H, W, 4), gbgra)
     assert cnt.medium_calls > 0
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_scene_check_accepts(name):
+    _, d, _, _ = _setup(name)
+    world = sio.ArrayScene(d)
+    stack_need, _ = sio.scene_check(world)
+    assert 0 < stack_need <= 48  # the exact-order kernel's call frames (XDEPTH)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_matches_reference(gpu_ctx, name):
+    c, d, ocam, op = _setup(name)
+    W, H = c["width"], c["height"]
+    world = sio.ArrayScene(d)
+    gpu_ctx.upload(world)
+    bgra, lin, st = gpu_ctx.render(rtow.camera_main(W, H), rtow.params(W, H, c["spp"], seed=c["seed"]))
+    glin, gbgra = sio.golden_image(name, W, H)
+    a = np.asarray(lin, np.float64).reshape(-1, 3)
+    rms = np.sqrt(np.mean((a - glin.reshape(-1, 3)) ** 2, axis=0))
+    exact = float(np.mean(lin.reshape(glin.shape) == glin))
+    print(f"{name}: rms {rms} exact {exact:.4f}")
+    assert (rms <= 1e-4).all(), rms
+    assert np.mean(bgra != gbgra) < 0.01
+    _, _, cnt = sio.oracle_render(world.view_ptr, ocam, op)
+    assert st.segments == cnt.segments

@@ -95,15 +95,14 @@ def test_medium_under_bvh_accepted(tmp_path):
     assert rtow.lib().rtow_scene_check(ctypes.addressof(arr.view), None, None) == rtow.OK
 
 
-def test_medium_under_bvh_behind_instance_rejected(tmp_path):
-    """...but not behind an instance or list there (the interval and frame the
-    medium would see are not replayed): refused loudly."""
+def test_medium_under_bvh_behind_instance_accepted(tmp_path):
+    """...and behind an instance or list there too: no program replays the
+    interval and frame such a medium sees, so the world goes to the
+    exact-order kernel (MODE 6, xhit; GPU parity: tests/test_medium_exact.py)."""
     import ctypes
 
     arr = _medium_under_bvh(tmp_path, True)
-    rc = rtow.lib().rtow_scene_check(ctypes.addressof(arr.view), None, None)
-    assert rc == rtow.E_UNSUPPORTED
-    assert b"instance or a list" in rtow.lib().rtow_last_error()
+    assert rtow.lib().rtow_scene_check(ctypes.addressof(arr.view), None, None) == rtow.OK
 
 
 def _save(s, tmp_path):
