@@ -44,6 +44,17 @@
 #include "rtow_device_layout.h"
 #include "rtow_internal.h"
 
+// Work stealing in the simple-scene traversal (trace_simple_ws)
+#ifndef RTOW_WS
+#define RTOW_WS 1
+#endif
+#ifndef RTOW_WS_MIN  // idle lanes a wave waits for before it steals
+#define RTOW_WS_MIN 1
+#endif
+#ifndef RTOW_WS_REFRESH  // a lane re-reads its ray's slot when it pops
+#define RTOW_WS_REFRESH 1
+#endif
+
 using namespace rtow_dev;
 
 // Device code lives in a named namespace so that one kernel instantiation can
@@ -791,6 +802,254 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
     return best;
 }
 
+// A BvhNode of unit-time spheres inside a general scene (TOP_SPHERES: a
+// top-level item that is a chain of instances over one), traversed in a loop
+// of its own: dnode_step's node step on the DNode twins (spheres inline, the
+// exact (x - o) * (1/d) slab planes of the general kernels), trace_simple's
+// register stack top, no kind dispatch.  `r` is the ray in the spheres' frame,
+// inv its reciprocals, a = dot(d, d), ra = 1 / a; bt / best the record so far
+// (the list's closest hit), updated with the reference's tie rule (tie keys).
+template <int STACK>
+__device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, const Ray& r, const F3& inv, float a,
+                                             float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk,
+                                             uint32_t& overflow) {
+    const uint32_t NONE = mkref(DK_NONE, 0);
+    SlabRay q;
+    q.o = r.o;
+    q.inv = inv;
+    bool found = false;
+    uint32_t cur = mkref(DK_BVH, root), top = NONE;
+    int sp = 0;
+    float btc = cull_bound(bt);
+    while (true) {
+        const float4* np = reinterpret_cast<const float4*>(S.node + (cur & INDEX_MASK));
+        const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
+        const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
+        float tb = 0.0f, ta = 0.0f;
+        bool hb = false, ha = false;
+        if ((refb >> KIND_SHIFT) == DK_SPHERE) {  // slot b (the right child) first
+            const F3 c = add(f3(b0.x, b0.y, b0.z), scl(r.time, f3(b1.x, b1.y, b1.z)));
+            float t;
+            if (sph_root(c, b0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refb, best)))) {
+                bt = t;
+                btc = cull_bound(t);
+                best = refb;
+                found = true;
+            }
+        } else {
+            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
+        }
+        if ((refa >> KIND_SHIFT) == DK_SPHERE) {
+            const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
+            float t;
+            if (sph_root(c, a0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refa, best)))) {
+                bt = t;
+                btc = cull_bound(t);
+                best = refa;
+                found = true;
+            }
+        } else {
+            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
+        }
+        const bool afirst = ta <= tb;
+        const bool both = ha && hb;
+        uint32_t nxt = both ? (afirst ? refa : refb) : (ha ? refa : (hb ? refb : NONE));
+        if (both) {
+            if (top != NONE) {
+                if (sp < STACK) {
+                    stk[sp * BLOCK] = top;
+                    sp++;
+                } else {
+                    overflow = 1;
+                }
+            }
+            top = afirst ? refb : refa;
+        }
+        if (nxt == NONE) {
+            nxt = top;
+            top = NONE;
+            if (sp > 0) {
+                --sp;
+                top = stk[sp * BLOCK];
+            }
+        }
+        if (nxt == NONE) break;
+        cur = nxt;
+    }
+    return found;
+}
+
+// Work stealing inside a wave (the simple-scene kernel; RTOW_WS).  A wave
+// steps trace_simple's loop until its last lane is done: with one ray per
+// lane, about half the lane-steps of a wave were idle lanes waiting (52 %
+// SIMD efficiency per step).  Here a lane whose traversal is over takes the
+// bottom entry of another lane's stack -- the oldest deferred subtree, the
+// largest -- and traverses it for THAT lane's ray (ray and slab constants
+// fetched with lane shuffles).  Every lane publishes the best hit it finds
+// for a ray in an LDS slot of the ray's lane, as a 64-bit key ordered like
+// sph_closer (t, then the larger leaf index on an exact tie): an atomic min,
+// so the closest hit is the minimum over everything any lane tested,
+// whichever lanes tested it.  The closest hit is a property of the leaves,
+// not of the visit order (DESIGN.md "The tree"), and culling only ever uses a
+// real hit of the same ray, so the frame is the same bit for bit.  Thieves
+// re-read the slot when they pop, so a donor's hits keep culling their work.
+__device__ __forceinline__ unsigned long long hit_key(float t, uint32_t ref) {
+    return ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(uint32_t)~ref;  // t > 0
+}
+template <int STACK, int BS>
+__device__ __forceinline__ uint32_t trace_simple_ws(const DevScene& S, const DNode* nodes, uint32_t root, const Ray& r_own,
+                                                    float tmin, float& bt_io, uint32_t* stk, unsigned long long* slots,
+                                                    uint32_t* wscratch, uint32_t& overflow) {
+    const uint32_t NONE = mkref(DK_NONE, 0);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wbase = threadIdx.x - lane;  // this wave's first thread of the block
+    // set bits of a wave mask below this lane
+    auto below = [](unsigned long long m) -> uint32_t {
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
+    Ray r = r_own;
+    SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
+    float a = dot(r.d, r.d);
+    float ra = 1.0f / a;
+    float bt = bt_io;
+    uint32_t best = NONE;
+    if ((root >> KIND_SHIFT) == DK_SPHERE) {
+        float t;
+        if (sph_t<true>(load_sph(S.sph + (root & INDEX_MASK)), r, a, ra, tmin, bt, t)) {
+            bt_io = t;
+            return root;
+        }
+        return best;
+    }
+    slots[threadIdx.x] = hit_key(bt, best);
+    uint32_t owner = threadIdx.x;  // the block thread whose ray this lane traverses
+    uint32_t cur = root, top = NONE;
+    int sp = 0, bot = 0;  // this lane's deferred entries in LDS: [bot, sp)
+    float btc = cull_bound(bt);
+    while (true) {
+        // ---- lanes whose traversal is over take other lanes' deferred subtrees
+        const unsigned long long idle = __ballot(cur == NONE);
+        if (idle && (__popcll(idle) >= RTOW_WS_MIN || idle == __ballot(1))) {
+            const unsigned long long donors = __ballot(sp > bot);
+            if (donors == 0) {
+                if (idle == __ballot(1)) break;  // every lane done, nothing deferred
+            } else {
+                const uint32_t n = min((uint32_t)__popcll(idle), (uint32_t)__popcll(donors));
+                const uint32_t rd = below(donors), ri = below(idle);
+                const bool give = sp > bot && rd < n;
+                const bool take = cur == NONE && ri < n;
+                if (give) wscratch[wbase + rd] = lane;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const int donor = take ? (int)wscratch[wbase + ri] : (int)lane;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // the donor's deferred entry, ray and owner (each shuffle merged
+                // at once: no set of shuffled values stays live)
+                const int dbot = __shfl(bot, donor);
+                const uint32_t downer = (uint32_t)__shfl((int)owner, donor);
+                float v;
+                v = __shfl(r.o.x, donor);
+                r.o.x = take ? v : r.o.x;
+                v = __shfl(r.o.y, donor);
+                r.o.y = take ? v : r.o.y;
+                v = __shfl(r.o.z, donor);
+                r.o.z = take ? v : r.o.z;
+                v = __shfl(r.d.x, donor);
+                r.d.x = take ? v : r.d.x;
+                v = __shfl(r.d.y, donor);
+                r.d.y = take ? v : r.d.y;
+                v = __shfl(r.d.z, donor);
+                r.d.z = take ? v : r.d.z;
+                v = __shfl(r.time, donor);
+                r.time = take ? v : r.time;
+                if (give) bot++;
+                if (take) {
+                    cur = stk[(ptrdiff_t)dbot * BS + donor - (int)lane];
+                    owner = downer;
+                    // the same per-ray constants the donor computed from the same ray
+                    q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
+                    a = dot(r.d, r.d);
+                    ra = 1.0f / a;
+                    const unsigned long long k = slots[owner];
+                    bt = __uint_as_float((uint32_t)(k >> 32));
+                    best = ~(uint32_t)k;
+                    btc = cull_bound(bt);
+                    sp = bot = 0;
+                    top = NONE;
+                }
+            }
+        }
+        if (cur != NONE) {
+            const float4* np = reinterpret_cast<const float4*>(nodes + (cur & INDEX_MASK));
+            const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
+            const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
+            float tb = 0.0f, ta = 0.0f;
+            bool hb = false, ha = false, took = false;
+            if ((refb >> KIND_SHIFT) == DK_SPHERE) {  // slot b (the right child) first
+                const F3 c = add(f3(b0.x, b0.y, b0.z), scl(r.time, f3(b1.x, b1.y, b1.z)));
+                float t;
+                if (sph_closer(c, b0.w, r, a, ra, tmin, bt, best, refb, t)) {
+                    bt = t;
+                    btc = cull_bound(t);
+                    best = refb;
+                    took = true;
+                }
+            } else {
+                hb = slab_f(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
+            }
+            if ((refa >> KIND_SHIFT) == DK_SPHERE) {
+                const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
+                float t;
+                if (sph_closer(c, a0.w, r, a, ra, tmin, bt, best, refa, t)) {
+                    bt = t;
+                    btc = cull_bound(t);
+                    best = refa;
+                    took = true;
+                }
+            } else {
+                ha = slab_f(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
+            }
+            if (took) atomicMin(&slots[owner], hit_key(bt, best));
+            const bool afirst = ta <= tb;
+            const bool both = ha && hb;
+            uint32_t nxt = both ? (afirst ? refa : refb) : (ha ? refa : (hb ? refb : NONE));
+            if (both) {  // push the farther child; the old top goes to LDS
+                if (top != NONE) {
+                    if (sp < STACK) {
+                        stk[sp * BS] = top;
+                        sp++;
+                    } else {
+                        overflow = 1;  // reported as an error by the host
+                    }
+                }
+                top = afirst ? refb : refa;
+            }
+            if (nxt == NONE) {  // pop (the slot may hold a nearer hit another lane found)
+                nxt = top;
+                top = NONE;
+                if (sp > bot) {
+                    --sp;
+                    top = stk[sp * BS];
+                }
+                if (sp == bot) sp = bot = 0;
+                const unsigned long long k = RTOW_WS_REFRESH ? slots[owner] : ~0ull;
+                if (k < hit_key(bt, best)) {
+                    bt = __uint_as_float((uint32_t)(k >> 32));
+                    best = ~(uint32_t)k;
+                    btc = cull_bound(bt);
+                }
+            }
+            cur = nxt;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long k = slots[threadIdx.x];
+    bt_io = __uint_as_float((uint32_t)(k >> 32));
+    return ~(uint32_t)k;
+}
+
 struct Best {
     float t;
     uint32_t prim;  // the leaf; its instance chain is the leaf's own (DSphere::chain ...)
@@ -1174,6 +1433,8 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
                 bp = mkref(DK_MEDIUM, T.a);
                 found = true;
             }
+        } else if (T.kind == TOP_SPHERES) {
+            if (trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow)) found = true;
         } else if (T.kind == TOP_SPHERE) {
             const uint32_t ref = mkref(DK_SPHERE, T.a);
             const Sph sp = load_sph(S.sph + T.a);
@@ -1255,6 +1516,241 @@ __device__ __forceinline__ void finalize(const DevScene& S, uint32_t prim, float
         root_out(S, rec.p, rec.n);
     else
         chain_out(S, chain, rec.p, rec.n);
+}
+
+// ---------------------------------------------------------------------------
+// MODE 6: worlds whose random draws depend on the reference's exact visit
+// order in ways the culled traversals cannot replay -- a ConstantMedium whose
+// boundary holds a medium (constantMedium.h:26-31 asks its boundary twice,
+// and asking a medium draws), or a medium below a BvhNode behind an instance
+// or inside a list (bvhNode.h:66-96 visits both children exhaustively, and a
+// list hands each item its closest hit so far, hitableList.h:24-34).  xhit is
+// the reference's own recursion, hit() over the raw scene graph (XHit =
+// rtow_hitable), made iterative: one frame per pending call in private
+// memory, each with its interval, its ray (the frame it sits in) and the
+// record it holds; no culling, every call and draw in the reference's order.
+// The leaf tests are the shared ones (sph_quad, rect arithmetic of
+// rect_t_ax), so a record is what the other kernels produce for it.
+struct XFrame {
+    uint32_t h, phase;
+    float tmin, tmax;
+    float aux;       // LIST: closest hit so far; MEDIUM: the boundary's first hit
+    uint32_t auxi;   // LIST: next item; BVH: left child hit
+    uint32_t have;   // LIST: a record is held
+    Ray r;
+    Rec rec;        // LIST: the record so far; BVH: the left child's
+};
+
+__device__ __forceinline__ bool xaabb(const float* f, const Ray& r, float tmin, float tmax) {  // aabb.h:22-43
+    return ref_slab(f[0], f[3], r.o.x, r.d.x, tmin, tmax) && ref_slab(f[1], f[4], r.o.y, r.d.y, tmin, tmax) &&
+           ref_slab(f[2], f[5], r.o.z, r.d.z, tmin, tmax);
+}
+
+template <int K, int I, int J>
+__device__ __forceinline__ bool xrect(const XHit& H, const Ray& r, float t0, float t1, Rec& rec) {  // xy_rect.h
+    const float t = (H.f[4] - cmp3<K>(r.o)) / cmp3<K>(r.d);
+    if (t < t0 || t > t1) return false;
+    const float x = cmp3<I>(r.o) + t * cmp3<I>(r.d);
+    const float y = cmp3<J>(r.o) + t * cmp3<J>(r.d);
+    if (x < H.f[0] || x > H.f[1] || y < H.f[2] || y > H.f[3]) return false;
+    rec.u = (x - H.f[0]) / (H.f[1] - H.f[0]);
+    rec.v = (y - H.f[2]) / (H.f[3] - H.f[2]);
+    rec.t = t;
+    rec.mat = H.a;
+    rec.p = at(r, t);
+    rec.n = f3(K == 0 ? 1.0f : 0.0f, K == 1 ? 1.0f : 0.0f, K == 2 ? 1.0f : 0.0f);
+    return true;
+}
+
+// The closest hit of the world for ray `wr` (world frame) in (tmin, FLT_MAX),
+// as color.h:17 asks for it; false: nothing hit (or the frames ran out:
+// `overflow`).
+__device__ __forceinline__ bool xhit(const DevScene& S, const Ray& wr, float tmin, Rng& rng, Rec& out,
+                                     uint32_t& overflow) {
+    XFrame fr[XDEPTH];
+    int d = 0;
+    bool rh = false;  // the result a finished call hands its caller
+    Rec rr;
+    rr.t = rr.u = rr.v = 0.0f;
+    rr.p = rr.n = f3(0, 0, 0);
+    rr.mat = 0;
+    auto call = [&](uint32_t h, const Ray& r, float t0, float t1) {
+        if (d >= XDEPTH) {
+            overflow = 1;
+            rh = false;
+            return;
+        }
+        XFrame& F = fr[d++];
+        F.h = h;
+        F.phase = 0;
+        F.tmin = t0;
+        F.tmax = t1;
+        F.r = r;
+    };
+    call(S.xroot, wr, tmin, FLT_MAX);
+    while (d > 0) {
+        XFrame& F = fr[d - 1];
+        const XHit& H = S.xh[F.h];
+        const uint32_t ph = F.phase;
+        switch (H.kind) {
+        case RTOW_HIT_SPHERE:
+        case RTOW_HIT_MOVING_SPHERE: {  // sphere.h:20-69, 93-118
+            const bool mv = H.kind == RTOW_HIT_MOVING_SPHERE;
+            const F3 c = mv ? add(ld3(H.f), scl((F.r.time - H.f[6]) / (H.f[7] - H.f[6]), sub(ld3(H.f + 3), ld3(H.f))))
+                            : ld3(H.f);
+            const float R = mv ? H.f[8] : H.f[3];
+            const float a = dot(F.r.d, F.r.d);
+            float t;
+            rh = sph_quad(c, R, F.r, a, 1.0f / a, F.tmin, F.tmax, t);
+            if (rh) {
+                rr.t = t;
+                rr.p = at(F.r, t);
+                const F3 pc = sub(rr.p, c);
+                rr.n = f3(pc.x / R, pc.y / R, pc.z / R);
+                rr.mat = H.a;
+                rr.u = rr.v = 0.0f;
+                if (!mv && S.mat[H.a].needs_uv) sphere_uv(rr.n, rr.u, rr.v);
+            }
+            d--;
+            break;
+        }
+        case RTOW_HIT_RECT_XY:
+            rh = xrect<2, 0, 1>(H, F.r, F.tmin, F.tmax, rr);
+            d--;
+            break;
+        case RTOW_HIT_RECT_XZ:
+            rh = xrect<1, 0, 2>(H, F.r, F.tmin, F.tmax, rr);
+            d--;
+            break;
+        case RTOW_HIT_RECT_YZ:
+            rh = xrect<0, 1, 2>(H, F.r, F.tmin, F.tmax, rr);
+            d--;
+            break;
+        case RTOW_HIT_BOX:  // box.h:43-45: its list of sides
+        case RTOW_HIT_FLIP_NORMALS:
+        case RTOW_HIT_TRANSLATE:
+        case RTOW_HIT_ROTATE_Y:
+            if (ph == 0) {  // hitable.h:25-154: the child with the moved ray
+                F.phase = 1;
+                Ray q = F.r;
+                if (H.kind == RTOW_HIT_TRANSLATE) {
+                    q.o = sub(F.r.o, ld3(H.f));
+                } else if (H.kind == RTOW_HIT_ROTATE_Y) {
+                    const float sn = H.f[0], cs = H.f[1];
+                    q.o.x = cs * F.r.o.x - sn * F.r.o.z;
+                    q.o.z = sn * F.r.o.x + cs * F.r.o.z;
+                    q.d.x = cs * F.r.d.x - sn * F.r.d.z;
+                    q.d.z = sn * F.r.d.x + cs * F.r.d.z;
+                }
+                call(H.a, q, F.tmin, F.tmax);
+            } else {  // the record on the way out
+                if (rh) {
+                    if (H.kind == RTOW_HIT_FLIP_NORMALS) {
+                        rr.n = neg(rr.n);
+                    } else if (H.kind == RTOW_HIT_TRANSLATE) {
+                        rr.p = add(rr.p, ld3(H.f));
+                    } else if (H.kind == RTOW_HIT_ROTATE_Y) {
+                        const float sn = H.f[0], cs = H.f[1];
+                        const F3 p = rr.p, n = rr.n;
+                        rr.p.x = cs * p.x + sn * p.z;
+                        rr.p.z = -sn * p.x + cs * p.z;
+                        rr.n.x = cs * n.x + sn * n.z;
+                        rr.n.z = -sn * n.x + cs * n.z;
+                    }
+                }
+                d--;
+            }
+            break;
+        case RTOW_HIT_LIST:  // hitableList.h:20-38
+            if (ph == 0) {
+                F.phase = 1;
+                F.aux = F.tmax;  // closestHitSoFar (a double holding float values)
+                F.auxi = 0;
+                F.have = 0;
+            } else if (rh) {
+                F.aux = rr.t;
+                F.rec = rr;
+                F.have = 1;
+            }
+            if (F.auxi < H.b) {
+                const uint32_t item = S.xrefs[H.a + F.auxi];
+                F.auxi++;
+                call(item, F.r, F.tmin, F.aux);
+            } else {
+                rh = F.have != 0;
+                if (rh) rr = F.rec;
+                d--;
+            }
+            break;
+        case RTOW_HIT_BVH_NODE:  // bvhNode.h:66-96
+            if (ph == 0) {
+                if (!xaabb(H.f, F.r, F.tmin, F.tmax)) {
+                    rh = false;
+                    d--;
+                    break;
+                }
+                F.phase = 1;
+                call(H.a, F.r, F.tmin, F.tmax);
+            } else if (ph == 1) {
+                F.auxi = rh ? 1u : 0u;
+                F.rec = rr;
+                F.phase = 2;
+                call(H.b, F.r, F.tmin, F.tmax);
+            } else {
+                if (F.auxi && rh) {
+                    if (F.rec.t < rr.t) rr = F.rec;
+                } else if (F.auxi) {
+                    rr = F.rec;
+                    rh = true;
+                }
+                d--;
+            }
+            break;
+        case RTOW_HIT_CONSTANT_MEDIUM:  // constantMedium.h:26-74
+            if (ph == 0) {
+                (void)rng.next();  // the discarded `db` draw
+                F.phase = 1;
+                call(H.a, F.r, -FLT_MAX, FLT_MAX);
+            } else if (ph == 1) {
+                if (!rh) {
+                    d--;
+                    break;
+                }
+                F.aux = rr.t;
+                F.phase = 2;
+                call(H.a, F.r, (float)((double)rr.t + 0.0001), FLT_MAX);
+            } else {
+                if (rh) {
+                    float ta = F.aux, tb = rr.t;
+                    rh = false;
+                    if (ta < F.tmin) ta = F.tmin;
+                    if (tb > F.tmax) tb = F.tmax;
+                    if (!(ta >= tb)) {
+                        if (ta < 0) ta = 0;
+                        const float dl = len(F.r.d);
+                        const float inside = (tb - ta) * dl;
+                        const float dist = (float)(-(1 / H.f[0]) * log(rng.next()));
+                        if (dist < inside) {
+                            rr.t = ta + dist / dl;
+                            rr.p = at(F.r, rr.t);
+                            rr.n = f3(1, 0, 0);
+                            rr.mat = H.b;
+                            rr.u = rr.v = 0.0f;
+                            rh = true;
+                        }
+                    }
+                }
+                d--;
+            }
+            break;
+        default:
+            rh = false;
+            d--;
+            break;
+        }
+    }
+    out = rr;
+    return rh;
 }
 
 // ---------------------------------------------------------------------------
@@ -1693,10 +2189,13 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
 // words: the path state the traversal does not read, parked while it runs
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
+// (simple scenes, RTOW_WS) the work-stealing slots: a 64-bit best-hit key and
+// a scratch word per thread (trace_simple_ws).
 constexpr int COLD = 12;
+
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
-           (general ? (size_t)COLD * BS * 4 : 0);
+           (general ? (size_t)COLD * BS * 4 : (RTOW_WS ? (size_t)BS * 12 : 0));
 }
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
@@ -1716,12 +2215,18 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         s_perm[i] = S.perm[i];
     }
     const DNode* nodes = S.node;
+    unsigned char* ws_base = smem + 5120 + (size_t)STACK * BS * 4;  // simple scenes: after the nodes (LDSN)
     if constexpr (SIMPLE && LDSN) {
         float4* s_node = reinterpret_cast<float4*>(smem + 5120 + (size_t)STACK * BS * 4);
         const float4* g = reinterpret_cast<const float4*>(S.node);
         for (uint32_t i = threadIdx.x; i < S.n_node * 4u; i += BS) s_node[i] = g[i];
         nodes = reinterpret_cast<const DNode*>(s_node);
+        ws_base += (size_t)S.n_node * sizeof(DNode);
     }
+    unsigned long long* ws_slots = reinterpret_cast<unsigned long long*>(ws_base);
+    uint32_t* ws_scratch = reinterpret_cast<uint32_t*>(ws_base + (size_t)BS * 8);
+    (void)ws_slots;
+    (void)ws_scratch;
     __syncthreads();
     const Tables T{s_ranvec, s_perm};
     uint32_t* stk = s_stack + threadIdx.x;
@@ -1797,7 +2302,13 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             }
             const Ray lray = root_ray(S, ray);
             float bt = FLT_MAX;
+#if RTOW_WS
+            const uint32_t prim = PROF ? trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof)
+                                       : trace_simple_ws<STACK, BS>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, ws_slots,
+                                                                   ws_scratch, overflow);
+#else
             const uint32_t prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
+#endif
             hit = (prim >> KIND_SHIFT) != DK_NONE;
             if constexpr (PROF) {
                 const unsigned long long t_now = __builtin_amdgcn_s_memtime();
@@ -1810,6 +2321,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 prof.cyc_fin += t_now - t_mark;
                 t_mark = t_now;
             }
+        } else if constexpr (MODE == 6) {
+            hit = xhit(S, ray, 0.001f, rng, rec, overflow);
         } else {
             // park the path state the traversal does not need (COLD)
             cold[0 * BS] = __float_as_uint(acc.x);
@@ -2029,6 +2542,7 @@ __global__ void assemble_kernel(uint32_t W, uint32_t H, uint32_t world, uint32_t
     RTOW_K_COMMON(X, M, 16) RTOW_K_PROF(X, M, 16) RTOW_K_COMMON(X, M, 20) RTOW_K_PROF(X, M, 20)   \
     RTOW_K_COMMON(X, M, 32) RTOW_K_PROF(X, M, 32) RTOW_K_DEEP(X, M)
 #define RTOW_K_HOT(X) X(0, 16, 4, false, 512, true, false)
+#define RTOW_KLIST_6(X) RTOW_K_COMMON(X, 6, 16) RTOW_K_PROF(X, 6, 16)
 #if defined(RTOW_TU_SIMPLE)
 #define RTOW_KX(M, S, W, P, B, L, D) template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
 RTOW_K_HOT(RTOW_KX)
@@ -2036,6 +2550,8 @@ RTOW_K_HOT(RTOW_KX)
 #define RTOW_KX(M, S, W, P, B, L, D) template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
 #if RTOW_TU_KERNELS == 0
 RTOW_KLIST_0(RTOW_KX)
+#elif RTOW_TU_KERNELS == 6
+RTOW_KLIST_6(RTOW_KX)
 #else
 RTOW_KLIST_G(RTOW_KX, RTOW_TU_KERNELS)
 #endif
@@ -2048,6 +2564,7 @@ RTOW_KLIST_G(RTOW_KX, 2)
 RTOW_KLIST_G(RTOW_KX, 3)
 RTOW_KLIST_G(RTOW_KX, 4)
 RTOW_KLIST_G(RTOW_KX, 5)
+RTOW_KLIST_6(RTOW_KX)
 #endif
 #undef RTOW_KX
 
@@ -2109,7 +2626,68 @@ struct HostLayout {
     std::vector<DProg> prog;         // DevScene::prog
     std::vector<DBox6> box6;         // DevScene::box6
     float tshift[3] = {0.0f, 0.0f, 0.0f};  // DevScene::tshift
+    // exact-order worlds (MODE 6, xhit): the raw scene graph
+    bool exact = false;
+    std::vector<XHit> xh;
+    std::vector<uint32_t> xrefs;
+    uint32_t xroot = 0;
 };
+
+// The deepest hit() recursion the reference runs over the raw graph (xhit's
+// frames: every call in flight, medium boundary queries included); 0 on a
+// cycle or beyond XDEPTH.
+uint32_t rawDepth(const rtow_scene& s, uint32_t h, std::vector<int>& memo, int guard = 0) {
+    if (h >= s.n_hitables || guard > XDEPTH) return XDEPTH + 1;
+    if (memo[h] > 0) return (uint32_t)memo[h];
+    if (memo[h] < 0) return XDEPTH + 1;  // on the current path: a cycle
+    memo[h] = -1;
+    const rtow_hitable& H = s.hitables[h];
+    uint32_t below = 0;
+    switch (H.kind) {
+    case RTOW_HIT_LIST:
+        for (uint32_t j = 0; j < H.b; j++) below = std::max(below, rawDepth(s, s.refs[H.a + j], memo, guard + 1));
+        break;
+    case RTOW_HIT_BVH_NODE:
+        below = std::max(rawDepth(s, H.a, memo, guard + 1), rawDepth(s, H.b, memo, guard + 1));
+        break;
+    case RTOW_HIT_FLIP_NORMALS:
+    case RTOW_HIT_TRANSLATE:
+    case RTOW_HIT_ROTATE_Y:
+    case RTOW_HIT_BOX:
+    case RTOW_HIT_CONSTANT_MEDIUM:
+        below = rawDepth(s, H.a, memo, guard + 1);
+        break;
+    default:
+        break;
+    }
+    memo[h] = (int)std::min<uint32_t>(below + 1, XDEPTH + 1);
+    return (uint32_t)memo[h];
+}
+
+static_assert(sizeof(XHit) == sizeof(rtow_hitable), "XHit mirrors rtow_hitable");
+int buildExact(const rtow_scene& s, HostLayout& L) {
+    for (uint32_t i = 0; i < s.n_hitables; i++) {
+        const rtow_hitable& h = s.hitables[i];
+        const bool child = h.kind == RTOW_HIT_FLIP_NORMALS || h.kind == RTOW_HIT_TRANSLATE ||
+                           h.kind == RTOW_HIT_ROTATE_Y || h.kind == RTOW_HIT_BOX || h.kind == RTOW_HIT_CONSTANT_MEDIUM;
+        if (child && h.a >= s.n_hitables) return set_error(RTOW_E_INVALID, "child index out of range");
+        if (h.kind == RTOW_HIT_BVH_NODE && (h.a >= s.n_hitables || h.b >= s.n_hitables))
+            return set_error(RTOW_E_INVALID, "BvhNode child out of range");
+    }
+    for (uint32_t j = 0; j < s.n_refs; j++)
+        if (s.refs[j] >= s.n_hitables) return set_error(RTOW_E_INVALID, "list entry out of range");
+    std::vector<int> memo(s.n_hitables, 0);
+    const uint32_t depth = rawDepth(s, s.root, memo);
+    if (depth > (uint32_t)XDEPTH)
+        return set_error(RTOW_E_UNSUPPORTED, "scene graph deeper than " + std::to_string(XDEPTH) + " calls (or cyclic)");
+    L.exact = true;
+    L.xh.resize(s.n_hitables);
+    std::memcpy(L.xh.data(), s.hitables, sizeof(XHit) * s.n_hitables);
+    L.xrefs.assign(s.refs, s.refs + s.n_refs);
+    L.xroot = s.root;
+    L.stack_need = depth;
+    return RTOW_OK;
+}
 
 // ---------------------------------------------------------------------------
 // Exact ties in general scenes.  The reference returns, among the leaves hit
@@ -2620,15 +3198,41 @@ struct GeneralSah {
     // from the reference graph before this), and a medium only sees the
     // nearest hit of the items before it (hitableList.h:30), which the run's
     // tree gives it as the scan did.  Media keep their places.
+    // An instance chain over a BvhNode of unit-time spheres with many leaves
+    // (final_ned's cloud) stays an item of its own: at the top level it is a
+    // TOP_SPHERES item (trace_dnodes) instead of a leaf of the run's tree.
+    bool sphereInstance(uint32_t ref) const {
+        uint32_t r = ref;
+        int n = 0;
+        for (; n < 64; n++) {
+            const uint32_t k = r >> KIND_SHIFT;
+            if (k != DK_TRANSLATE && k != DK_ROTY && k != DK_FLIP) break;
+            r = L.inst[r & INDEX_MASK].child;
+        }
+        return n > 0 && (r >> KIND_SHIFT) == DK_BVH && onlyUnitSpheres(r) && leafCount(r) >= 16;
+    }
+    bool onlyUnitSpheres(uint32_t ref, int depth = 0) const {
+        const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+        if (depth > 200) return false;
+        if (kind == DK_SPHERE) return L.sph[idx].t0 == 0.0f && L.sph[idx].t1 == 1.0f;
+        if (kind != DK_BVH) return false;
+        return onlyUnitSpheres(L.bvh[idx].left, depth + 1) && onlyUnitSpheres(L.bvh[idx].right, depth + 1);
+    }
+
     void treeRuns(const DList& l) {
         std::vector<uint32_t> items(L.refs.begin() + l.first, L.refs.begin() + l.first + l.count), out;
         size_t j = 0;
         while (j < items.size()) {
             std::vector<GenLeaf> run;
+            std::vector<uint32_t> alone;  // sphereInstance items of the run
             size_t k = j;
             for (; k < items.size(); k++) {
                 GenLeaf g;
                 if (hasMedium(items[k]) || !bounds(items[k], g.mn, g.mx)) break;
+                if (sphereInstance(items[k])) {
+                    alone.push_back(items[k]);
+                    continue;
+                }
                 for (int a = 0; a < 3; a++) g.c[a] = 0.5f * (g.mn[a] + g.mx[a]);
                 g.ref = items[k];
                 run.push_back(g);
@@ -2638,8 +3242,9 @@ struct GeneralSah {
             if (run.size() >= 2 && big >= 16) {
                 out.push_back(sahBuildBvh(run, 0, run.size(), L.bvh));
             } else {
-                for (size_t q = j; q < k; q++) out.push_back(items[q]);
+                for (const GenLeaf& g : run) out.push_back(g.ref);
             }
+            for (uint32_t a : alone) out.push_back(a);
             if (k < items.size()) out.push_back(items[k]);  // the barrier item
             j = k + 1;
         }
@@ -3252,6 +3857,10 @@ void buildTop(HostLayout& L) {
             t = DTop{TOP_SPHERE, i, 0, L.sph[i].chain};
         } else if (k == DK_MEDIUM && L.med[i].bkind != MB_ANY) {
             t = DTop{TOP_MEDIUM, i, 0, L.med[i].chain};
+        } else if (k == DK_BVH && leaf != item && GeneralSah{L, 0}.sphereInstance(item)) {
+            uint32_t s0 = leaf;  // any leaf sphere gives the chain of the frame they share
+            while ((s0 >> KIND_SHIFT) == DK_BVH) s0 = L.bvh[s0 & INDEX_MASK].left;
+            t = DTop{TOP_SPHERES, i, 0, L.sph[s0 & INDEX_MASK].chain};
         }
         L.top.push_back(t);
     }
@@ -3330,7 +3939,6 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     if (!cv.err.empty()) return set_error(RTOW_E_UNSUPPORTED, cv.err);
     Bounds bd{L};
     auto nb = bd.need(L.root, false);
-    if (bd.mediaInBoundary) return set_error(RTOW_E_UNSUPPORTED, "ConstantMedium inside a medium boundary");
     L.stack_need = nb.first;
     L.chain_need = nb.second;
     if (L.chain_need > (uint32_t)MAXCHAIN)
@@ -3432,17 +4040,23 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         std::vector<uint32_t> path;
         refAncestors(L, L.root, path);
     }
-    if (!L.simple && tree == RTOW_TREE_SAH) {  // after the tie keys: they come from the reference trees
+    // A medium inside a medium's boundary: the culled traversals cannot ask it
+    // in the reference's order -- the world goes to the exact-order kernel
+    bool exact = bd.mediaInBoundary;
+    if (!exact && !L.simple && tree == RTOW_TREE_SAH) {  // after the tie keys: they come from the reference trees
         GeneralSah g{L, (uint32_t)L.bvh.size()};
         g.patch(L.root);
         Bounds bd2{L};
         L.stack_need = bd2.need(L.root, false).first;
     }
-    if (!L.simple) {  // BvhNode subtrees with media: replayed programs (DK_PROG)
+    if (!exact && !L.simple) {  // BvhNode subtrees with media: replayed programs (DK_PROG)
         ProgramBuilder pb{L};
         pb.patch(L.root);
-        if (!pb.err.empty()) return set_error(RTOW_E_UNSUPPORTED, pb.err);
-        if (!L.prog.empty()) {
+        // a medium below a BvhNode behind an instance or inside a list: no
+        // program replays it (a list hands it its own closest hit so far) --
+        // the exact-order kernel does
+        if (!pb.err.empty()) exact = true;
+        if (!exact && !L.prog.empty()) {
             Bounds bd3{L};
             L.stack_need = bd3.need(L.root, false).first;
         }
@@ -3474,9 +4088,13 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         }
         if (M.bkind == MB_ANY) L.media_any = true;
     }
-    if (!L.simple && tree == RTOW_TREE_SAH) {
+    if (!exact && !L.simple && tree == RTOW_TREE_SAH) {
         buildTop(L);
         buildGeneralNodes(L);
+    }
+    if (exact) {
+        const int rc = buildExact(s, L);
+        if (rc) return rc;
     }
     // media the top-level scan does not ask (TOP_MEDIUM) are asked inside the
     // general traversal
@@ -3510,6 +4128,7 @@ struct rtow_context {
     int waves = 4;  // trace-kernel occupancy variant (RTOW_TRACE_WAVES; 4 measured best, tools/probe.py)
     int profile = 0;  // RTOW_PROFILE=1: instrumented trace kernel, counters printed to stderr
     int lds_nodes = 1;  // simple-scene BVH staged in LDS when it fits (RTOW_LDS_NODES=0 disables; +11%, tools/ab.py)
+    uint32_t auto_spc = 16;  // samples per work item under automatic chunking (RTOW_AUTO_SPC)
     int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
     // rtow_debug_trace_sample (a render with the segment-recording kernel)
     float* dbg_out = nullptr;
@@ -3621,6 +4240,7 @@ int launchStack(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
 
 int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const DevScene& d = c->scene;
+    if (d.exact) return launchWaves<6, 16>(c, cam, P, bpc, st);
     if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
     if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
     if (!d.media_any && !d.media_nested) return launchStack<5>(c, cam, P, bpc, st);
@@ -3638,7 +4258,7 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     P.width = p->width;
     P.height = p->height;
     P.spp = p->spp;
-    uint32_t spc = p->samples_per_chunk ? p->samples_per_chunk : 16;  // short items keep the grid's tail short (tools/rank_share.py)
+    uint32_t spc = p->samples_per_chunk ? p->samples_per_chunk : c->auto_spc;  // short items keep the grid's tail short (tools/rank_share.py)
     if (spc > p->spp) spc = p->spp;
     P.n_chunks = (p->spp + spc - 1) / spc;
     if (P.n_chunks > 200 && !p->samples_per_chunk) {
@@ -3829,6 +4449,7 @@ int rtow_context_create(int device, rtow_context** out) {
     if (const char* w = std::getenv("RTOW_TRACE_WAVES")) c->waves = std::atoi(w);
     if (const char* pr = std::getenv("RTOW_PROFILE")) c->profile = std::atoi(pr);
     if (const char* ln = std::getenv("RTOW_LDS_NODES")) c->lds_nodes = std::atoi(ln);
+    if (const char* sc = std::getenv("RTOW_AUTO_SPC")) c->auto_spc = std::max(1, std::atoi(sc));
     if (const char* tr = std::getenv("RTOW_BVH")) c->tree = std::string(tr) == "ref" ? RTOW_TREE_REFERENCE : RTOW_TREE_SAH;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
@@ -3903,6 +4524,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_prog = pushBlob(blob, L.prog);
     if (L.box6.empty()) L.box6.push_back(DBox6{});
     size_t o_box6 = pushBlob(blob, L.box6);
+    if (L.xh.empty()) L.xh.push_back(XHit{});
+    if (L.xrefs.empty()) L.xrefs.push_back(0u);
+    size_t o_xh = pushBlob(blob, L.xh), o_xrefs = pushBlob(blob, L.xrefs);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -3951,6 +4575,10 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.n_node = L.simple ? (uint32_t)L.node.size() : 0u;
     d.gnode = L.gnode ? 1u : 0u;
     d.media_nested = L.media_nested ? 1u : 0u;
+    d.xh = (const XHit*)(b + o_xh);
+    d.xrefs = (const uint32_t*)(b + o_xrefs);
+    d.xroot = L.xroot;
+    d.exact = L.exact ? 1u : 0u;
     c->has_scene = true;
     // progressive sums belong to the scene they were rendered from: a new
     // scene restarts them (rtow_render_progressive)

@@ -167,8 +167,12 @@ struct alignas(16) DProg {  // 32 B; lo/hi read as ref_aabb_hit's (min xyz, -, m
 // the ray in the leaf's frame); a medium whose boundary is a sphere or a
 // Box's rectangles (MB_SPHERE / MB_RECTS) is asked right there (TOP_MEDIUM,
 // with the closest hit so far as its tmax, hitableList.h:30); anything else
-// goes to the general traversal.
-enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2, TOP_MEDIUM = 3, TOP_BOX6 = 4 };  // BOX6: a = box6 index
+// goes to the general traversal -- except a chain of instances over a BvhNode
+// of unit-time spheres only (final_ned's cloud, Translate(RotateY(BvhNode of
+// 1000 spheres))): TOP_SPHERES runs its DNode tree in a loop of its own
+// (trace_dnodes) in the leaves' frame, entered once per ray.
+enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2, TOP_MEDIUM = 3, TOP_BOX6 = 4, TOP_SPHERES = 5 };
+// BOX6: a = box6 index; SPHERES: a = the DNode index of the BvhNode
 struct alignas(16) DTop {  // 16 B
     uint32_t kind;
     uint32_t a;      // GENERIC: item ref; RECTS: first rectangle; SPHERE: sphere; MEDIUM: medium
@@ -241,6 +245,21 @@ struct DevScene {
     uint32_t n_node;         // DNode count (simple scenes)
     float tshift[3];         // simple scenes: world-frame offset of the DNode boxes (shiftBoxes)
     uint32_t gnode;          // general scene: node[i] is the DNode twin of bvh[i] (DK_BVH steps read it)
+    // exact-order worlds (MODE 6): the scene graph as the reference builds
+    // it, one XHit per rtow_hitable (include/rtow.h), interpreted by xhit
+    const struct XHit* xh;
+    const uint32_t* xrefs;
+    uint32_t xroot;
+    uint32_t exact;
 };
+
+// One reference Hitable, as rtow_hitable (include/rtow.h) lays it out.
+struct alignas(16) XHit {  // 64 B
+    uint32_t kind, a, b, c;
+    float f[12];
+};
+// The deepest reference hit() recursion xhit follows (frames in private
+// memory); deeper worlds are refused at upload.
+constexpr int XDEPTH = 48;
 
 }  // namespace rtow_dev
