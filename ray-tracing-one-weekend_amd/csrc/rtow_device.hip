@@ -44,16 +44,6 @@
 #include "rtow_device_layout.h"
 #include "rtow_internal.h"
 
-// Work stealing in the simple-scene traversal (trace_simple_ws)
-#ifndef RTOW_WS
-#define RTOW_WS 1
-#endif
-#ifndef RTOW_WS_MIN  // idle lanes a wave waits for before it steals
-#define RTOW_WS_MIN 1
-#endif
-#ifndef RTOW_WS_REFRESH  // a lane re-reads its ray's slot when it pops
-#define RTOW_WS_REFRESH 1
-#endif
 
 using namespace rtow_dev;
 
@@ -120,8 +110,10 @@ struct DevCam {
 // for auto chunking, a tail of R = spp - n_big*spc samples (spc <= R < 2 spc)
 // cut into halving chunks: tail chunk k holds samples
 // [base + R - L(k), base + R - L(k+1)), L(k) = ceil(R / 2^k), L(n_tail) = 0 --
-// R = 16 gives 8, 4, 2, 1, 1.  Items run chunk-major, so the grid ends on
-// one-sample items instead of spc-sample ones: a short tail at every rank count.
+// R = 16 gives 8, 4, 2, 1, 1.  The n_big full chunks run pixel-major (item =
+// pixel * n_big + chunk), the tail chunk-major after them, so the grid ends
+// on one-sample items instead of spc-sample ones: a short tail at every rank
+// count.
 struct DevParams {
     uint32_t width, height, spp, spc;  // spc: samples per chunk
     uint32_t n_chunks, n_local_px, tiles_x, rank, world;
@@ -877,177 +869,6 @@ __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, c
         cur = nxt;
     }
     return found;
-}
-
-// Work stealing inside a wave (the simple-scene kernel; RTOW_WS).  A wave
-// steps trace_simple's loop until its last lane is done: with one ray per
-// lane, about half the lane-steps of a wave were idle lanes waiting (52 %
-// SIMD efficiency per step).  Here a lane whose traversal is over takes the
-// bottom entry of another lane's stack -- the oldest deferred subtree, the
-// largest -- and traverses it for THAT lane's ray (ray and slab constants
-// fetched with lane shuffles).  Every lane publishes the best hit it finds
-// for a ray in an LDS slot of the ray's lane, as a 64-bit key ordered like
-// sph_closer (t, then the larger leaf index on an exact tie): an atomic min,
-// so the closest hit is the minimum over everything any lane tested,
-// whichever lanes tested it.  The closest hit is a property of the leaves,
-// not of the visit order (DESIGN.md "The tree"), and culling only ever uses a
-// real hit of the same ray, so the frame is the same bit for bit.  Thieves
-// re-read the slot when they pop, so a donor's hits keep culling their work.
-__device__ __forceinline__ unsigned long long hit_key(float t, uint32_t ref) {
-    return ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(uint32_t)~ref;  // t > 0
-}
-template <int STACK, int BS>
-__device__ __forceinline__ uint32_t trace_simple_ws(const DevScene& S, const DNode* nodes, uint32_t root, const Ray& r_own,
-                                                    float tmin, float& bt_io, uint32_t* stk, unsigned long long* slots,
-                                                    uint32_t* wscratch, uint32_t& overflow) {
-    const uint32_t NONE = mkref(DK_NONE, 0);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wbase = threadIdx.x - lane;  // this wave's first thread of the block
-    // set bits of a wave mask below this lane
-    auto below = [](unsigned long long m) -> uint32_t {
-        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    };
-    Ray r = r_own;
-    SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
-    float a = dot(r.d, r.d);
-    float ra = 1.0f / a;
-    float bt = bt_io;
-    uint32_t best = NONE;
-    if ((root >> KIND_SHIFT) == DK_SPHERE) {
-        float t;
-        if (sph_t<true>(load_sph(S.sph + (root & INDEX_MASK)), r, a, ra, tmin, bt, t)) {
-            bt_io = t;
-            return root;
-        }
-        return best;
-    }
-    slots[threadIdx.x] = hit_key(bt, best);
-    uint32_t owner = threadIdx.x;  // the block thread whose ray this lane traverses
-    uint32_t cur = root, top = NONE;
-    int sp = 0, bot = 0;  // this lane's deferred entries in LDS: [bot, sp)
-    float btc = cull_bound(bt);
-    while (true) {
-        // ---- lanes whose traversal is over take other lanes' deferred subtrees
-        const unsigned long long idle = __ballot(cur == NONE);
-        if (idle && (__popcll(idle) >= RTOW_WS_MIN || idle == __ballot(1))) {
-            const unsigned long long donors = __ballot(sp > bot);
-            if (donors == 0) {
-                if (idle == __ballot(1)) break;  // every lane done, nothing deferred
-            } else {
-                const uint32_t n = min((uint32_t)__popcll(idle), (uint32_t)__popcll(donors));
-                const uint32_t rd = below(donors), ri = below(idle);
-                const bool give = sp > bot && rd < n;
-                const bool take = cur == NONE && ri < n;
-                if (give) wscratch[wbase + rd] = lane;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                const int donor = take ? (int)wscratch[wbase + ri] : (int)lane;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                // the donor's deferred entry, ray and owner (each shuffle merged
-                // at once: no set of shuffled values stays live)
-                const int dbot = __shfl(bot, donor);
-                const uint32_t downer = (uint32_t)__shfl((int)owner, donor);
-                float v;
-                v = __shfl(r.o.x, donor);
-                r.o.x = take ? v : r.o.x;
-                v = __shfl(r.o.y, donor);
-                r.o.y = take ? v : r.o.y;
-                v = __shfl(r.o.z, donor);
-                r.o.z = take ? v : r.o.z;
-                v = __shfl(r.d.x, donor);
-                r.d.x = take ? v : r.d.x;
-                v = __shfl(r.d.y, donor);
-                r.d.y = take ? v : r.d.y;
-                v = __shfl(r.d.z, donor);
-                r.d.z = take ? v : r.d.z;
-                v = __shfl(r.time, donor);
-                r.time = take ? v : r.time;
-                if (give) bot++;
-                if (take) {
-                    cur = stk[(ptrdiff_t)dbot * BS + donor - (int)lane];
-                    owner = downer;
-                    // the same per-ray constants the donor computed from the same ray
-                    q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
-                    a = dot(r.d, r.d);
-                    ra = 1.0f / a;
-                    const unsigned long long k = slots[owner];
-                    bt = __uint_as_float((uint32_t)(k >> 32));
-                    best = ~(uint32_t)k;
-                    btc = cull_bound(bt);
-                    sp = bot = 0;
-                    top = NONE;
-                }
-            }
-        }
-        if (cur != NONE) {
-            const float4* np = reinterpret_cast<const float4*>(nodes + (cur & INDEX_MASK));
-            const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
-            const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
-            float tb = 0.0f, ta = 0.0f;
-            bool hb = false, ha = false, took = false;
-            if ((refb >> KIND_SHIFT) == DK_SPHERE) {  // slot b (the right child) first
-                const F3 c = add(f3(b0.x, b0.y, b0.z), scl(r.time, f3(b1.x, b1.y, b1.z)));
-                float t;
-                if (sph_closer(c, b0.w, r, a, ra, tmin, bt, best, refb, t)) {
-                    bt = t;
-                    btc = cull_bound(t);
-                    best = refb;
-                    took = true;
-                }
-            } else {
-                hb = slab_f(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
-            }
-            if ((refa >> KIND_SHIFT) == DK_SPHERE) {
-                const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
-                float t;
-                if (sph_closer(c, a0.w, r, a, ra, tmin, bt, best, refa, t)) {
-                    bt = t;
-                    btc = cull_bound(t);
-                    best = refa;
-                    took = true;
-                }
-            } else {
-                ha = slab_f(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
-            }
-            if (took) atomicMin(&slots[owner], hit_key(bt, best));
-            const bool afirst = ta <= tb;
-            const bool both = ha && hb;
-            uint32_t nxt = both ? (afirst ? refa : refb) : (ha ? refa : (hb ? refb : NONE));
-            if (both) {  // push the farther child; the old top goes to LDS
-                if (top != NONE) {
-                    if (sp < STACK) {
-                        stk[sp * BS] = top;
-                        sp++;
-                    } else {
-                        overflow = 1;  // reported as an error by the host
-                    }
-                }
-                top = afirst ? refb : refa;
-            }
-            if (nxt == NONE) {  // pop (the slot may hold a nearer hit another lane found)
-                nxt = top;
-                top = NONE;
-                if (sp > bot) {
-                    --sp;
-                    top = stk[sp * BS];
-                }
-                if (sp == bot) sp = bot = 0;
-                const unsigned long long k = RTOW_WS_REFRESH ? slots[owner] : ~0ull;
-                if (k < hit_key(bt, best)) {
-                    bt = __uint_as_float((uint32_t)(k >> 32));
-                    best = ~(uint32_t)k;
-                    btc = cull_bound(bt);
-                }
-            }
-            cur = nxt;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const unsigned long long k = slots[threadIdx.x];
-    bt_io = __uint_as_float((uint32_t)(k >> 32));
-    return ~(uint32_t)k;
 }
 
 struct Best {
@@ -2189,13 +2010,11 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
 // words: the path state the traversal does not read, parked while it runs
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
-// (simple scenes, RTOW_WS) the work-stealing slots: a 64-bit best-hit key and
-// a scratch word per thread (trace_simple_ws).
 constexpr int COLD = 12;
 
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
-           (general ? (size_t)COLD * BS * 4 : (RTOW_WS ? (size_t)BS * 12 : 0));
+           (general ? (size_t)COLD * BS * 4 : 0);
 }
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
@@ -2215,18 +2034,12 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         s_perm[i] = S.perm[i];
     }
     const DNode* nodes = S.node;
-    unsigned char* ws_base = smem + 5120 + (size_t)STACK * BS * 4;  // simple scenes: after the nodes (LDSN)
     if constexpr (SIMPLE && LDSN) {
         float4* s_node = reinterpret_cast<float4*>(smem + 5120 + (size_t)STACK * BS * 4);
         const float4* g = reinterpret_cast<const float4*>(S.node);
         for (uint32_t i = threadIdx.x; i < S.n_node * 4u; i += BS) s_node[i] = g[i];
         nodes = reinterpret_cast<const DNode*>(s_node);
-        ws_base += (size_t)S.n_node * sizeof(DNode);
     }
-    unsigned long long* ws_slots = reinterpret_cast<unsigned long long*>(ws_base);
-    uint32_t* ws_scratch = reinterpret_cast<uint32_t*>(ws_base + (size_t)BS * 8);
-    (void)ws_slots;
-    (void)ws_scratch;
     __syncthreads();
     const Tables T{s_ranvec, s_perm};
     uint32_t* stk = s_stack + threadIdx.x;
@@ -2257,8 +2070,21 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 const uint32_t rank = (uint32_t)__popcll(want & ((1ull << lane) - 1ull));
                 item = base + rank;
                 if (item >= P.n_items) break;
-                const uint32_t chunk = item / P.n_local_px;
-                const uint32_t lp = item - chunk * P.n_local_px;
+                // the n_big full chunks pixel-major (a pixel's chunks run side
+                // by side: their sums meet in L2 instead of each evicting the
+                // pixel's line), then the halving tail chunk-major (the grid
+                // ends on one-sample items)
+                uint32_t chunk, lp;
+                const uint32_t nb_items = P.n_big * P.n_local_px;
+                if (item < nb_items) {
+                    lp = item / P.n_big;
+                    chunk = item - lp * P.n_big;
+                } else {
+                    const uint32_t j = item - nb_items;
+                    const uint32_t k = j / P.n_local_px;
+                    lp = j - k * P.n_local_px;
+                    chunk = P.n_big + k;
+                }
                 uint32_t x, yimg;
                 if (!decode_pixel(P, lp, x, yimg)) continue;  // padding pixel of a partial tile
                 lpx = lp;
@@ -2302,13 +2128,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             }
             const Ray lray = root_ray(S, ray);
             float bt = FLT_MAX;
-#if RTOW_WS
-            const uint32_t prim = PROF ? trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof)
-                                       : trace_simple_ws<STACK, BS>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, ws_slots,
-                                                                   ws_scratch, overflow);
-#else
             const uint32_t prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
-#endif
             hit = (prim >> KIND_SHIFT) != DK_NONE;
             if constexpr (PROF) {
                 const unsigned long long t_now = __builtin_amdgcn_s_memtime();
@@ -4128,7 +3948,7 @@ struct rtow_context {
     int waves = 4;  // trace-kernel occupancy variant (RTOW_TRACE_WAVES; 4 measured best, tools/probe.py)
     int profile = 0;  // RTOW_PROFILE=1: instrumented trace kernel, counters printed to stderr
     int lds_nodes = 1;  // simple-scene BVH staged in LDS when it fits (RTOW_LDS_NODES=0 disables; +11%, tools/ab.py)
-    uint32_t auto_spc = 16;  // samples per work item under automatic chunking (RTOW_AUTO_SPC)
+    uint32_t auto_spc = 0;  // samples per work item under automatic chunking (RTOW_AUTO_SPC; 0: from the grid, makeParams)
     int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
     // rtow_debug_trace_sample (a render with the segment-recording kernel)
     float* dbg_out = nullptr;
@@ -4258,7 +4078,25 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     P.width = p->width;
     P.height = p->height;
     P.spp = p->spp;
-    uint32_t spc = p->samples_per_chunk ? p->samples_per_chunk : c->auto_spc;  // short items keep the grid's tail short (tools/rank_share.py)
+    // Automatic chunking: the longest items (fewer refills and pixel-sum
+    // atomics: 64 samples are 4.6 % faster than 16 on config 2) that still
+    // leave >= 64 items per lane of the grid (cus x 1024 lanes), so a rank's
+    // share of a multi-GPU frame keeps a short tail (config 2 over 8 ranks:
+    // 16-sample items 0.927 of the ideal, 64-sample 0.877; tools/rank_share.py).
+    // RTOW_AUTO_SPC (c->auto_spc) fixes the length instead.
+    const uint32_t n_px = rtow_rank_tile_count(p->width, p->height, p->rank, world) * 64u;
+    uint32_t spc = p->samples_per_chunk;
+    if (!spc && c->auto_spc) spc = c->auto_spc;
+    if (!spc) {
+        const uint64_t lanes = (uint64_t)std::max(1, c->cus) * 1024u;
+        spc = 16;
+        for (uint32_t cand : {64u, 32u}) {
+            if ((uint64_t)n_px * ((p->spp + cand - 1) / cand) >= 64 * lanes) {
+                spc = cand;
+                break;
+            }
+        }
+    }
     if (spc > p->spp) spc = p->spp;
     P.n_chunks = (p->spp + spc - 1) / spc;
     if (P.n_chunks > 200 && !p->samples_per_chunk) {
