@@ -23,8 +23,9 @@ import codeobj  # noqa: E402
 LIB = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "librtow_hip.so")
 
 # scratch bytes per lane allowed for the default (4-wave) general kernels,
-# by MODE (see DESIGN.md "Kernels"); the simple-scene kernels get none
-SCRATCH_BOUND = {0: 0, 2: 0, 4: 64, 3: 160, 5: 24}
+# by MODE (see DESIGN.md "Kernels"); the simple-scene kernels get none; the
+# exact-order kernel (MODE 6) keeps its call frames in scratch (48 x 96 B)
+SCRATCH_BOUND = {0: 0, 2: 0, 4: 64, 3: 160, 5: 24, 6: 48 * 96 + 64}
 
 
 @pytest.fixture(scope="module")
@@ -57,7 +58,7 @@ def test_default_kernels_scratch_bounded(kernels):
         seen.add(p["MODE"])
         assert k["scratch"] <= SCRATCH_BOUND[p["MODE"]], (p, k["scratch"])
         assert k["vgpr"] <= 128, p
-    assert seen == {0, 2, 3, 4, 5}
+    assert seen == {0, 2, 3, 4, 5, 6}
 
 
 def test_each_kernel_compiled_once(kernels):
@@ -66,4 +67,4 @@ def test_each_kernel_compiled_once(kernels):
     names = [k["name"] for k in kernels]
     assert len(names) == len(set(names))
     modes = {codeobj.demangled_params(n)["MODE"] for n in names if codeobj.demangled_params(n)}
-    assert modes == {0, 2, 3, 4, 5}
+    assert modes == {0, 2, 3, 4, 5, 6}
