@@ -52,7 +52,7 @@ using namespace rtow_dev;
 // flags (RTOW_TU_SIMPLE, see the Makefile and the end of this section).
 namespace rtow_k {
 
-// Block size of every general-scene kernel: the general traversal (bvh_step,
+// Block size of every general-scene kernel: the general traversal (dnode_step,
 // traverse) strides a lane's LDS stack column by BLOCK, so a general kernel
 // must be instantiated with BS == BLOCK (static_assert in trace_kernel); only
 // the simple-scene traversal (trace_simple) takes the block size as BS.
@@ -573,66 +573,13 @@ __device__ __forceinline__ bool first_active_lane() {
 }
 
 // ---------------------------------------------------------------------------
-// One BvhNode step (bvhNode.h:66-96 semantics): both child boxes are tested;
-// sphere children are tested right here (right child first, so that on an
-// exact tie the right one wins, as bvhNode.h:74-77 decides); of the inner
-// children that are hit the nearer is returned and the farther pushed.
-// Returns the next node to visit, or DK_NONE to pop.
-template <bool UNIT_TIME, int STACK>
-__device__ __forceinline__ uint32_t bvh_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
-                                             float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
-                                             uint32_t& overflow) {
-    // `best`: in, the current closest leaf; out, the winner of this step's spheres
-    const DBvh* n = S.bvh + idx;
-    const float4 xs = reinterpret_cast<const float4*>(n)[0];
-    const float4 ys = reinterpret_cast<const float4*>(n)[1];
-    const float4 zs = reinterpret_cast<const float4*>(n)[2];
-    const uint4 lr = reinterpret_cast<const uint4*>(n)[3];
-    float tl, tr;
-    const float btc = cull_bound(bt);
-    const bool hl = slab(xs.x, xs.y, ys.x, ys.y, zs.x, zs.y, q, tmin, btc, tl);
-    const bool hr = slab(xs.z, xs.w, ys.z, ys.w, zs.z, zs.w, q, tmin, btc, tr);
-    const bool lleaf = (lr.x >> KIND_SHIFT) == DK_SPHERE;
-    const bool rleaf = (lr.y >> KIND_SHIFT) == DK_SPHERE;
-    if (hr && rleaf) {
-        float t;
-        const Sph sp1 = load_sph(S.sph + (lr.y & INDEX_MASK));
-        if (sph_root(sph_center<UNIT_TIME>(sp1, r.time), sp1.r, r, a, ra, tmin, t) &&
-            (t < bt || (t == bt && wins_tie(S, lr.y, best)))) {
-            bt = t;
-            best = lr.y;
-        }
-    }
-    if (hl && lleaf) {
-        float t;
-        const Sph sp0 = load_sph(S.sph + (lr.x & INDEX_MASK));
-        if (sph_root(sph_center<UNIT_TIME>(sp0, r.time), sp0.r, r, a, ra, tmin, t) &&
-            (t < bt || (t == bt && wins_tie(S, lr.x, best)))) {
-            bt = t;
-            best = lr.x;
-        }
-    }
-    const bool li = hl && !lleaf, ri = hr && !rleaf;
-    if (li && ri) {
-        const bool lfirst = tl <= tr;
-        if (sp < STACK) {
-            stk[sp * BLOCK] = lfirst ? lr.y : lr.x;
-            sp++;
-        } else {
-            overflow = 1;
-        }
-        return lfirst ? lr.x : lr.y;
-    }
-    if (li) return lr.x;
-    if (ri) return lr.y;
-    return mkref(DK_NONE, 0);
-}
-
-// The DK_BVH step of a general scene in SAH mode (DevScene::gnode): the
-// node's DNode twin, sphere children inline (tested right here, no box test
-// and no second fetch), any other child a box slot.  Same contract as
-// bvh_step: the nearer hit inner child is returned, the farther pushed;
-// exact ties between leaves by the tie keys.
+// The DK_BVH step of a general scene (BvhNode semantics, bvhNode.h:66-96):
+// the node's DNode twin (DevScene::gnode: of the SAH tree, or of the
+// reference's own with RTOW_TREE_REFERENCE), unit-time sphere children inline
+// (tested right here, no box test and no second fetch: the closest hit of a
+// set of leaves does not depend on which boxes are tested first), any other
+// child a box slot; of the inner children that are hit the nearer is
+// returned and the farther pushed; exact ties between leaves by the tie keys.
 template <int STACK>
 __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
                                                float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
@@ -1022,10 +969,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
         if (kind == DK_BVH) {
             const uint32_t before = best.prim;
             uint32_t b = before;
-            const uint32_t nxt = S.gnode ? dnode_step<STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
-                                 : S.unit_time
-                                     ? bvh_step<true, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow)
-                                     : bvh_step<false, STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow);
+            const uint32_t nxt = dnode_step<STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow);
             if (b != before) {
                 best.prim = b;
                 found = true;
@@ -3908,9 +3852,9 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         }
         if (M.bkind == MB_ANY) L.media_any = true;
     }
-    if (!exact && !L.simple && tree == RTOW_TREE_SAH) {
-        buildTop(L);
-        buildGeneralNodes(L);
+    if (!exact && !L.simple) {
+        if (tree == RTOW_TREE_SAH) buildTop(L);
+        buildGeneralNodes(L);  // DNode twins of the SAH trees, or of the reference's own (RTOW_TREE_REFERENCE)
     }
     if (exact) {
         const int rc = buildExact(s, L);

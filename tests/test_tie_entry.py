@@ -12,6 +12,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 import scene_io as sio
 
@@ -46,3 +47,24 @@ def test_fixture_holds_the_culled_tie():
     red = (glin[..., 0] > 1.5 * glin[..., 1]) & (glin[..., 0] > 1.5 * glin[..., 2])
     green = (glin[..., 1] > 1.5 * glin[..., 0]) & (glin[..., 1] > 1.2 * glin[..., 2])
     assert red.sum() > 50 and green.sum() > 3
+
+
+@pytest.mark.gpu
+def test_gpu_matches_reference(gpu_ctx):
+    """The device settles the tie as the reference does (rect_reaches_tie:
+    the BvhNode boxes between the list and the rectangle, asked with the
+    list's closest hit so far): within the north-star bar, segment count equal."""
+    import rtow
+
+    c, d, ocam, op = setup()
+    W, H = c["width"], c["height"]
+    world = sio.ArrayScene(d)
+    gpu_ctx.upload(world)
+    bgra, lin, st = gpu_ctx.render(rtow.camera_main(W, H), rtow.params(W, H, c["spp"], seed=c["seed"]))
+    glin, gbgra = sio.golden_image("tie_bvh_entry", W, H)
+    a = np.asarray(lin, np.float64).reshape(-1, 3)
+    rms = np.sqrt(np.mean((a - glin.reshape(-1, 3)) ** 2, axis=0))
+    print(f"tie_bvh_entry: rms {rms} exact {float(np.mean(lin.reshape(glin.shape) == glin)):.4f}")
+    assert (rms <= 1e-4).all(), rms
+    _, _, cnt = sio.oracle_render(world.view_ptr, ocam, op)
+    assert st.segments == cnt.segments
