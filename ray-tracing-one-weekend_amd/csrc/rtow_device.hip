@@ -502,34 +502,28 @@ __device__ __forceinline__ bool ref_skips_hit(const DevScene& S, uint32_t rect, 
 
 // A Box's six sides (DBox6) in their list order (box.h:29-38), each tested as
 // the rectangle-list loop tests it: the interval [tmin, bt] shrinks as sides
-// are taken, exact ties go by the tie keys, and in strict mode a side counts
-// only where the reference's boxes reach it.  Returns whether a side was taken.
-__device__ __forceinline__ bool wins_tie(const DevScene& S, uint32_t cand, uint32_t best);
+// are taken, exact ties go by the tie keys.  Returns whether a side was taken.
+__device__ __forceinline__ bool take_hit(const DevScene& S, float t, float& bt, uint32_t& best, uint32_t cand);
 template <int K, int I, int J>
 __device__ __forceinline__ void box6_side(const DevScene& S, float a0, float a1, float b0, float b1, float k,
                                           uint32_t rect, const Ray& r, const F3& inv, float tmin, float& bt,
-                                          uint32_t& best, bool strict, bool& found) {
+                                          uint32_t& best, bool& found) {
     float t;
-    const uint32_t ref = mkref(DK_RECT, rect);
-    if (rect_t_ax<K, I, J>(a0, a1, b0, b1, k, r, inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, best)) &&
-        (!strict || ref_reaches_rect(S, rect, r, tmin))) {
-        bt = t;
-        best = ref;
+    if (rect_t_ax<K, I, J>(a0, a1, b0, b1, k, r, inv, tmin, bt, t) && take_hit(S, t, bt, best, mkref(DK_RECT, rect)))
         found = true;
-    }
 }
 __device__ __forceinline__ bool box6_scan(const DevScene& S, uint32_t bi, const Ray& r, const F3& inv, float tmin,
-                                          float& bt, uint32_t& best, bool strict) {
+                                          float& bt, uint32_t& best) {
     const float4 lo = reinterpret_cast<const float4*>(S.box6 + bi)[0];
     const float4 hi = reinterpret_cast<const float4*>(S.box6 + bi)[1];
     const uint32_t f = __float_as_uint(lo.w);
     bool found = false;
-    box6_side<2, 0, 1>(S, lo.x, hi.x, lo.y, hi.y, hi.z, f + 0, r, inv, tmin, bt, best, strict, found);  // XY at z1 (flipped)
-    box6_side<2, 0, 1>(S, lo.x, hi.x, lo.y, hi.y, lo.z, f + 1, r, inv, tmin, bt, best, strict, found);  // XY at z0
-    box6_side<1, 0, 2>(S, lo.x, hi.x, lo.z, hi.z, hi.y, f + 2, r, inv, tmin, bt, best, strict, found);  // XZ at y1
-    box6_side<1, 0, 2>(S, lo.x, hi.x, lo.z, hi.z, lo.y, f + 3, r, inv, tmin, bt, best, strict, found);  // XZ at y0 (flipped)
-    box6_side<0, 1, 2>(S, lo.y, hi.y, lo.z, hi.z, hi.x, f + 4, r, inv, tmin, bt, best, strict, found);  // YZ at x1
-    box6_side<0, 1, 2>(S, lo.y, hi.y, lo.z, hi.z, lo.x, f + 5, r, inv, tmin, bt, best, strict, found);  // YZ at x0 (flipped)
+    box6_side<2, 0, 1>(S, lo.x, hi.x, lo.y, hi.y, hi.z, f + 0, r, inv, tmin, bt, best, found);  // XY at z1 (flipped)
+    box6_side<2, 0, 1>(S, lo.x, hi.x, lo.y, hi.y, lo.z, f + 1, r, inv, tmin, bt, best, found);  // XY at z0
+    box6_side<1, 0, 2>(S, lo.x, hi.x, lo.z, hi.z, hi.y, f + 2, r, inv, tmin, bt, best, found);  // XZ at y1
+    box6_side<1, 0, 2>(S, lo.x, hi.x, lo.z, hi.z, lo.y, f + 3, r, inv, tmin, bt, best, found);  // XZ at y0 (flipped)
+    box6_side<0, 1, 2>(S, lo.y, hi.y, lo.z, hi.z, hi.x, f + 4, r, inv, tmin, bt, best, found);  // YZ at x1
+    box6_side<0, 1, 2>(S, lo.y, hi.y, lo.z, hi.z, lo.x, f + 5, r, inv, tmin, bt, best, found);  // YZ at x0 (flipped)
     return found;
 }
 // ConstantMedium's boundary query over a Box (MB_BOX6): the nearest side hit
@@ -560,11 +554,66 @@ struct Prof {
 // General scenes: does leaf `cand`, hit at exactly the t of the current best
 // leaf `best`, take the record in the reference?  (assignTieKeys)
 __device__ __forceinline__ unsigned long long leaf_key(const DevScene& S, uint32_t ref) {
-    const uint32_t k = ref >> KIND_SHIFT, i = ref & INDEX_MASK;
+    const uint32_t k = ref >> KIND_SHIFT, i = ref & LEAF_MASK;
     return k == DK_SPHERE ? S.sph_key[i] : (k == DK_RECT ? S.rect_key[i] : (k == DK_MEDIUM ? S.med_key[i] : 0ull));
 }
-__device__ __forceinline__ bool wins_tie(const DevScene& S, uint32_t cand, uint32_t best) {
-    return (best >> KIND_SHIFT) == DK_NONE || leaf_key(S, cand) > leaf_key(S, best);
+// An exact tie at the record's t: does leaf `cand` take the record from
+// `best`?  The keys decide (the larger wins); the record keeps, in its tie
+// bits (TIE_MASK), the first key bit where the two leaves' paths part (+1):
+// tie_unsettled() checks after the traversal whether the reference's boxes
+// let the winner see that tie at all.
+__device__ __forceinline__ bool tie_pick(const DevScene& S, uint32_t cand, uint32_t& best) {
+    if ((best >> KIND_SHIFT) == DK_NONE) {
+        best = cand;
+        return true;
+    }
+    const unsigned long long kc = leaf_key(S, cand), kb = leaf_key(S, best);
+    const bool w = kc > kb;
+    const unsigned long long x = kc ^ kb;
+    const uint32_t info = x ? (uint32_t)__clzll((long long)x) + 1u : 0u;
+    best = ((w ? cand : best) & ~TIE_MASK) | (info << TIE_SHIFT);
+    return w;
+}
+// The record: a strictly nearer hit takes it, an exact tie goes by tie_pick.
+// True when `cand` holds the record afterwards.
+__device__ __forceinline__ bool take_hit(const DevScene& S, float t, float& bt, uint32_t& best, uint32_t cand) {
+    if (t < bt) {
+        bt = t;
+        best = cand;
+        return true;
+    }
+    return t == bt && tie_pick(S, cand, best);
+}
+
+// After a traversal: did the winning rectangle `prim` take or keep an exact
+// tie (its tie bits: the first key bit where the two leaves' paths part) that
+// the reference never lets it see?  Where the paths part at a HitableList,
+// the reference asks the later item with (tmin, t) -- the list's closest hit
+// so far (hitableList.h:24-34) -- and every BvhNode between the list and the
+// rectangle with that interval; AABB::hit rejects a box the ray enters exactly
+// at t (`tmax <= tmin`, aabb.h:22-43).  When a box below the list fails that
+// test, which item keeps the tie depends on the order the culled traversal
+// does not record: the ray is settled by xhit.  rect_lvl (assignTieKeys): per
+// list level on the rectangle's path, its key component's bits and how many
+// of the rectangle's reference boxes (rect_anc, its own frame) lie below it.
+__device__ __forceinline__ bool tie_unsettled(const DevScene& S, uint32_t prim, const Ray& wray, float tmin, float t) {
+    const uint32_t info = (prim & TIE_MASK) >> TIE_SHIFT;
+    if (!info) return false;
+    const uint32_t p = info - 1u, rect = prim & LEAF_MASK;
+    const uint32_t a = S.rect_anc[rect], cnt = a & 255u, off = a >> 8;
+    if (cnt == 0) return false;
+    for (int k = 0; k < 4; k++) {
+        const uint32_t lv = S.rect_lvl[4 * (size_t)rect + k];
+        if (!(lv >> 31)) break;
+        const uint32_t st = lv & 255u, w = (lv >> 8) & 255u, suf = min((lv >> 16) & 255u, cnt);
+        if (p < st || p >= st + w) continue;
+        if (suf == 0) return false;
+        const Ray rr = chain_ray(S, S.rect[rect].chain, wray);
+        for (uint32_t i = cnt - suf; i < cnt; i++)
+            if (!ref_aabb_hit(S.abox + 8 * (size_t)(off + i), rr, tmin, t)) return true;
+        return false;
+    }
+    return false;  // the paths part at a BvhNode: both children see the same interval
 }
 
 __device__ __forceinline__ bool first_active_lane() {
@@ -593,20 +642,14 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
     if ((refb >> KIND_SHIFT) == DK_SPHERE) {  // slot b (the right child) first
         const F3 c = add(f3(b0.x, b0.y, b0.z), scl(r.time, f3(b1.x, b1.y, b1.z)));
         float t;
-        if (sph_root(c, b0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refb, best)))) {
-            bt = t;
-            best = refb;
-        }
+        if (sph_root(c, b0.w, r, a, ra, tmin, t)) take_hit(S, t, bt, best, refb);
     } else {
         hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) != DK_NONE;
     }
     if ((refa >> KIND_SHIFT) == DK_SPHERE) {
         const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
         float t;
-        if (sph_root(c, a0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refa, best)))) {
-            bt = t;
-            best = refa;
-        }
+        if (sph_root(c, a0.w, r, a, ra, tmin, t)) take_hit(S, t, bt, best, refa);
     } else {
         ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) != DK_NONE;
     }
@@ -769,10 +812,8 @@ __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, c
         if ((refb >> KIND_SHIFT) == DK_SPHERE) {  // slot b (the right child) first
             const F3 c = add(f3(b0.x, b0.y, b0.z), scl(r.time, f3(b1.x, b1.y, b1.z)));
             float t;
-            if (sph_root(c, b0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refb, best)))) {
-                bt = t;
-                btc = cull_bound(t);
-                best = refb;
+            if (sph_root(c, b0.w, r, a, ra, tmin, t) && take_hit(S, t, bt, best, refb)) {
+                btc = cull_bound(bt);
                 found = true;
             }
         } else {
@@ -781,10 +822,8 @@ __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, c
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
             float t;
-            if (sph_root(c, a0.w, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, refa, best)))) {
-                bt = t;
-                btc = cull_bound(t);
-                best = refa;
+            if (sph_root(c, a0.w, r, a, ra, tmin, t) && take_hit(S, t, bt, best, refa)) {
+                btc = cull_bound(bt);
                 found = true;
             }
         } else {
@@ -858,7 +897,7 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
 template <bool MEDIA, int STACK, bool ANYB = true>
 __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin,
                                          float tmax, uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow,
-                                         uint32_t prev, bool strict = false, Prof* prof = nullptr);
+                                         uint32_t prev, Prof* prof = nullptr);
 
 template <int STACK, bool ANYB>
 __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, const Ray& wray,
@@ -947,7 +986,7 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
 template <bool MEDIA, int STACK, bool ANYB>
 __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const Ray& wray, uint32_t chain0, float tmin,
                                          float tmax, uint32_t* stk, int sp0, Rng& rng, Best& best, uint32_t& overflow,
-                                         uint32_t prev, bool strict, Prof* prof) {
+                                         uint32_t prev, Prof* prof) {
     Ray r = chain_ray(S, chain0, wray);
     SlabRay q = slab_ray(r);
     float a = dot(r.d, r.d);
@@ -982,36 +1021,22 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
             float t;
             const Sph s = load_sph(S.sph + idx);
             const F3 c = S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time);
-            const uint32_t ref = mkref(DK_SPHERE, idx);
-            if (sph_root(c, s.r, r, a, ra, tmin, t) &&
-                (t < bt || (t == bt && wins_tie(S, ref, best.prim)))) {
-                bt = t;
-                best.prim = ref;
+            if (sph_root(c, s.r, r, a, ra, tmin, t) && take_hit(S, t, bt, best.prim, mkref(DK_SPHERE, idx)))
                 found = true;
-            }
         } else if (kind == DK_RECT) {
             float t;
-            if (rect_t(S.rect[idx], r, q.inv, tmin, bt, t) && (t < bt || wins_tie(S, cur, best.prim)) &&
-                (!strict || ref_reaches_rect(S, idx, r, tmin))) {
-                bt = t;
-                best.prim = cur;
-                found = true;
-            }
+            if (rect_t(S.rect[idx], r, q.inv, tmin, bt, t) && take_hit(S, t, bt, best.prim, cur)) found = true;
         } else if (kind == DK_RECTS) {
             // a list of rectangles: scanned in order, closed interval, as hitableList.h
             const DList R = S.list[idx];
             if (R.box6) {  // a Box's sides: the unrolled scan
-                if (box6_scan(S, R.box6 - 1, r, q.inv, tmin, bt, best.prim, strict)) found = true;
+                if (box6_scan(S, R.box6 - 1, r, q.inv, tmin, bt, best.prim)) found = true;
             } else
             for (uint32_t j = 0; j < R.count; j++) {
-                const uint32_t ref = mkref(DK_RECT, R.first + j);
                 float t;
-                if (rect_t(S.rect[R.first + j], r, q.inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, best.prim)) &&
-                    (!strict || ref_reaches_rect(S, R.first + j, r, tmin))) {
-                    bt = t;
-                    best.prim = ref;
+                if (rect_t(S.rect[R.first + j], r, q.inv, tmin, bt, t) &&
+                    take_hit(S, t, bt, best.prim, mkref(DK_RECT, R.first + j)))
                     found = true;
-                }
             }
         } else if (kind == DK_LIST || kind == DK_LISTNEXT) {
             // items in order; one continuation entry below the item being
@@ -1106,11 +1131,8 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                 float tm = tmed == tmed ? tmed : bt;
                 tmed = __builtin_nanf("");
                 if (medium_hit<STACK, ANYB>(S, idx, r, a, wray, tmin, tm, stk, sp, rng, overflow) &&
-                    (tm < bt || (tm == bt && wins_tie(S, cur, best.prim)))) {
-                    bt = tm;
-                    best.prim = cur;
+                    take_hit(S, tm, bt, best.prim, cur))
                     found = true;
-                }
             }
         }
         if (sp == sp0) break;
@@ -1118,7 +1140,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
         cur = stk[sp * BLOCK];
     }
     best.t = bt;
-    return found;
+    return found || best.prim != prev;  // (an exact tie settled for `prev` marks its tie bits)
 }
 
 // The closest hit of a general scene whose root (below its instances) is a
@@ -1128,7 +1150,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
 // TOPMED: media as top-level items (TOP_MEDIUM).
 template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false>
 __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
-                             uint32_t& overflow, bool strict, Prof* prof = nullptr) {
+                             uint32_t& overflow, Prof* prof = nullptr) {
     float bt = FLT_MAX;
     uint32_t bp = mkref(DK_NONE, 0);
     bool found = false;
@@ -1151,7 +1173,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
         if (T.kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
             Best b;
-            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp, strict,
+            if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp,
                                              PROF ? prof : nullptr)) {
                 bt = b.t;
                 bp = b.prim;
@@ -1179,17 +1201,12 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             prof->cyc_chain += __builtin_amdgcn_s_memtime() - tc;
         }
         if (T.kind == TOP_BOX6) {
-            if (box6_scan(S, T.a, r, inv, tmin, bt, bp, strict)) found = true;
+            if (box6_scan(S, T.a, r, inv, tmin, bt, bp)) found = true;
         } else if (T.kind == TOP_RECTS) {
             for (uint32_t k = 0; k < T.b; k++) {
-                const uint32_t ref = mkref(DK_RECT, T.a + k);
                 float t;
-                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t) && (t < bt || wins_tie(S, ref, bp)) &&
-                    (!strict || ref_reaches_rect(S, T.a + k, r, tmin))) {
-                    bt = t;
-                    bp = ref;
+                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t) && take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k)))
                     found = true;
-                }
             }
         } else if (TOPMED && T.kind == TOP_MEDIUM) {
             // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
@@ -1201,15 +1218,10 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         } else if (T.kind == TOP_SPHERES) {
             if (trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow)) found = true;
         } else if (T.kind == TOP_SPHERE) {
-            const uint32_t ref = mkref(DK_SPHERE, T.a);
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
             float t;
-            if (sph_root(c, sp.r, r, a, ra, tmin, t) && (t < bt || (t == bt && wins_tie(S, ref, bp)))) {
-                bt = t;
-                bp = ref;
-                found = true;
-            }
+            if (sph_root(c, sp.r, r, a, ra, tmin, t) && take_hit(S, t, bt, bp, mkref(DK_SPHERE, T.a))) found = true;
         }
     }
     if constexpr (PROF) {
@@ -2103,34 +2115,32 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             cold[11 * BS] = depth;
             Best best;
             best.prim = 0;
-            // a winning rectangle the reference would not have reached (its
-            // boxes grazed at an edge): trace the ray again, this time testing
-            // every rectangle hit against the reference's boxes (same draws)
             const Rng rng0 = rng;
-            bool strict = false;
-            while (true) {
-                if constexpr (PROF) {
-                    const unsigned long long t_now = __builtin_amdgcn_s_memtime();
-                    prof.cyc_other += t_now - t_mark;
-                    t_mark = t_now;
-                }
-                hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF>(S, ray, 0.001f, stk, rng,
-                                                                                           best, overflow, strict,
-                                                                                           &prof);
-                if constexpr (PROF) {
-                    const unsigned long long t_now = __builtin_amdgcn_s_memtime();
-                    prof.cyc_trav += t_now - t_mark;
-                    t_mark = t_now;
-                }
-                if (!strict && hit && (best.prim >> KIND_SHIFT) == DK_RECT &&
-                    ref_skips_hit(S, best.prim & INDEX_MASK, ray, best.t, 0.001f)) {
-                    rng = rng0;
-                    strict = true;
-                    continue;
-                }
-                break;
+            if constexpr (PROF) {
+                const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                prof.cyc_other += t_now - t_mark;
+                t_mark = t_now;
             }
-            if (hit) finalize<false>(S, best.prim, best.t, ray, rec);
+            hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF>(S, ray, 0.001f, stk, rng, best,
+                                                                                       overflow, &prof);
+            if constexpr (PROF) {
+                const unsigned long long t_now = __builtin_amdgcn_s_memtime();
+                prof.cyc_trav += t_now - t_mark;
+                t_mark = t_now;
+            }
+            // A winning rectangle the reference would not have reached -- its
+            // boxes grazed at an edge (ref_skips_hit), or entered exactly at
+            // the t of a tie it won (tie_unsettled) -- and the record is the
+            // reference's only by its own recursion: the ray again, same
+            // draws, through xhit (the exact-order kernel's hit()).
+            if (hit && (best.prim >> KIND_SHIFT) == DK_RECT &&
+                (ref_skips_hit(S, best.prim & LEAF_MASK, ray, best.t, 0.001f) ||
+                 tie_unsettled(S, best.prim, ray, 0.001f, best.t))) {
+                rng = rng0;
+                hit = xhit(S, ray, 0.001f, rng, rec, overflow);
+            } else if (hit) {
+                finalize<false>(S, best.prim & ~TIE_MASK, best.t, ray, rec);
+            }
             acc = f3(__uint_as_float(cold[0 * BS]), __uint_as_float(cold[1 * BS]), __uint_as_float(cold[2 * BS]));
             thr = f3(__uint_as_float(cold[3 * BS]), __uint_as_float(cold[4 * BS]), __uint_as_float(cold[5 * BS]));
             lpx = cold[6 * BS];
@@ -2385,6 +2395,7 @@ struct HostLayout {
     // the node's own box (6 floats) in collapsed_own; AABB::hit still tests it
     std::vector<float> collapsed_own;
     std::unordered_map<uint32_t, uint32_t> collapsed_of;
+    std::vector<uint32_t> rect_lvl;  // DevScene::rect_lvl
     std::vector<uint32_t> rect_anc;  // DevScene::rect_anc
     std::vector<float> abox;         // DevScene::abox
     std::vector<DProg> prog;         // DevScene::prog
@@ -2557,9 +2568,18 @@ struct ChainAssigner {
 struct KeyComp {
     uint32_t bits;
     unsigned long long closed, open;
+    // list components: where refAncestors' in-frame box path stood when the
+    // list was entered (frame: which instance frame that was)
+    bool list = false;
+    uint32_t frame = 0, boxes = 0;
+};
+// refAncestors' box path as assignTieKeys walks the same graph: its length
+// in the current frame (a Translate / RotateY starts a new one)
+struct TieWalk {
+    uint32_t frame = 0, boxes = 0, next_frame = 1;
 };
 
-void assignTieKeys(HostLayout& L, uint32_t ref, std::vector<KeyComp>& path, int depth = 0) {
+void assignTieKeys(HostLayout& L, uint32_t ref, std::vector<KeyComp>& path, TieWalk& tw, int depth = 0) {
     if (depth > 512) return;
     const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
     auto key = [&](bool closed) {
@@ -2572,22 +2592,43 @@ void assignTieKeys(HostLayout& L, uint32_t ref, std::vector<KeyComp>& path, int 
         }
         return used ? k << (64 - used) : 0ull;
     };
+    // a rectangle's list levels (DevScene::rect_lvl, tie_unsettled): the
+    // innermost four, with how many boxes of its frame lie below each
+    auto levels = [&](uint32_t rect) {
+        std::vector<uint32_t> lv;
+        uint32_t at = 0;
+        for (const KeyComp& c : path) {
+            if (at + c.bits > 64) break;
+            if (c.list) {
+                const uint32_t below = c.frame == tw.frame ? tw.boxes - c.boxes : tw.boxes;
+                lv.push_back(at | (c.bits << 8) | (std::min(below, 255u) << 16) | 0x80000000u);
+            }
+            at += c.bits;
+        }
+        const size_t from = lv.size() > 4 ? lv.size() - 4 : 0;
+        for (size_t k = from; k < lv.size(); k++) L.rect_lvl[4 * (size_t)rect + (k - from)] = lv[k];
+    };
+    const bool collapsed = L.collapsed_of.count(ref) != 0;  // an n == 1 BvhNode's box (refAncestors)
+    if (collapsed) tw.boxes++;
     switch (kind) {
     case DK_SPHERE:
         L.sph_key[idx] = key(false);
         break;
     case DK_RECT:
         L.rect_key[idx] = key(true);
+        levels(idx);
         break;
     case DK_MEDIUM:
         L.med_key[idx] = key(false);
         break;
     case DK_BVH:
+        tw.boxes++;
         for (uint32_t c = 0; c < 2; c++) {
             path.push_back(KeyComp{1, c, c});
-            assignTieKeys(L, c ? L.bvh[idx].right : L.bvh[idx].left, path, depth + 1);
+            assignTieKeys(L, c ? L.bvh[idx].right : L.bvh[idx].left, path, tw, depth + 1);
             path.pop_back();
         }
+        tw.boxes--;
         break;
     case DK_LIST:
     case DK_RECTS: {
@@ -2595,20 +2636,31 @@ void assignTieKeys(HostLayout& L, uint32_t ref, std::vector<KeyComp>& path, int 
         uint32_t bits = 1;
         while ((1ull << bits) < 2ull * l.count) bits++;
         for (uint32_t j = 0; j < l.count; j++) {
-            path.push_back(KeyComp{bits, (unsigned long long)l.count + j, (unsigned long long)l.count - 1 - j});
-            assignTieKeys(L, kind == DK_RECTS ? mkref(DK_RECT, l.first + j) : L.refs[l.first + j], path, depth + 1);
+            path.push_back(KeyComp{bits, (unsigned long long)l.count + j, (unsigned long long)l.count - 1 - j, true,
+                                   tw.frame, tw.boxes});
+            assignTieKeys(L, kind == DK_RECTS ? mkref(DK_RECT, l.first + j) : L.refs[l.first + j], path, tw, depth + 1);
             path.pop_back();
         }
         break;
     }
-    case DK_TRANSLATE:
-    case DK_ROTY:
     case DK_FLIP:
-        assignTieKeys(L, L.inst[idx].child, path, depth + 1);
+        assignTieKeys(L, L.inst[idx].child, path, tw, depth + 1);
         break;
+    case DK_TRANSLATE:
+    case DK_ROTY: {
+        const TieWalk saved = tw;
+        tw.frame = tw.next_frame++;
+        tw.boxes = 0;
+        assignTieKeys(L, L.inst[idx].child, path, tw, depth + 1);
+        const uint32_t nf = tw.next_frame;
+        tw = saved;
+        tw.next_frame = nf;
+        break;
+    }
     default:
         break;
     }
+    if (collapsed) tw.boxes--;
 }
 
 // ---------------------------------------------------------------------------
@@ -3792,12 +3844,16 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         ca.walk(L.root);
         if (!ca.err.empty()) return set_error(RTOW_E_UNSUPPORTED, ca.err);
     }
+    if (L.sph.size() > LEAF_MASK || L.rect.size() > LEAF_MASK || L.med.size() > LEAF_MASK)
+        return set_error(RTOW_E_UNSUPPORTED, "more than 2^21 spheres, rectangles or media");
     L.sph_key.assign(L.sph.size(), 0ull);
     L.rect_key.assign(L.rect.size(), 0ull);
     L.med_key.assign(L.med.size(), 0ull);
+    L.rect_lvl.assign(4 * L.rect.size(), 0u);
     {
         std::vector<KeyComp> path;
-        assignTieKeys(L, L.root, path);
+        TieWalk tw;
+        assignTieKeys(L, L.root, path, tw);
     }
     L.rect_anc.assign(L.rect.size(), 0u);
     if (!L.simple) {  // the reference BvhNodes above each rectangle (before the trees are rebuilt)
@@ -3859,6 +3915,16 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     if (exact) {
         const int rc = buildExact(s, L);
         if (rc) return rc;
+    } else if (!L.simple) {
+        // the raw graph, for the rays whose record only the reference's own
+        // recursion settles (xhit after ref_skips_hit / tie_unsettled)
+        std::vector<int> memo(s.n_hitables, 0);
+        if (rawDepth(s, s.root, memo) > (uint32_t)XDEPTH)
+            return set_error(RTOW_E_UNSUPPORTED, "scene graph deeper than " + std::to_string(XDEPTH) + " calls (or cyclic)");
+        L.xh.resize(s.n_hitables);
+        std::memcpy(L.xh.data(), s.hitables, sizeof(XHit) * s.n_hitables);
+        L.xrefs.assign(s.refs, s.refs + s.n_refs);
+        L.xroot = s.root;
     }
     // media the top-level scan does not ask (TOP_MEDIUM) are asked inside the
     // general traversal
@@ -4301,7 +4367,8 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_top = pushBlob(blob, top);
     if (L.rect_anc.empty()) L.rect_anc.push_back(0u);
     if (L.abox.empty()) L.abox.assign(8, 0.0f);
-    size_t o_anc = pushBlob(blob, L.rect_anc), o_abox = pushBlob(blob, L.abox);
+    if (L.rect_lvl.size() < 4) L.rect_lvl.resize(4, 0u);
+    size_t o_anc = pushBlob(blob, L.rect_anc), o_abox = pushBlob(blob, L.abox), o_lvl = pushBlob(blob, L.rect_lvl);
     if (L.prog.empty()) L.prog.push_back(DProg{});
     size_t o_prog = pushBlob(blob, L.prog);
     if (L.box6.empty()) L.box6.push_back(DBox6{});
@@ -4342,6 +4409,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.n_top = (uint32_t)L.top.size();
     d.rect_anc = (const uint32_t*)(b + o_anc);
     d.abox = (const float*)(b + o_abox);
+    d.rect_lvl = (const uint32_t*)(b + o_lvl);
     d.prog = (const DProg*)(b + o_prog);
     d.box6 = (const DBox6*)(b + o_box6);
     for (int a = 0; a < 3; a++) d.tshift[a] = L.tshift[a];

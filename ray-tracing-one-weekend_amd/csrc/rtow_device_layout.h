@@ -42,6 +42,14 @@ enum : uint32_t {
 constexpr uint32_t KIND_SHIFT = 28;
 constexpr uint32_t INDEX_MASK = (1u << KIND_SHIFT) - 1;
 constexpr uint32_t mkref(uint32_t kind, uint32_t idx) { return (kind << KIND_SHIFT) | idx; }
+// A leaf reference held as a traversal's record (sphere, rectangle, medium)
+// carries tie bits above its index: the first key bit where it and the leaf
+// it tied with part (+1; 0: no exact tie), for tie_unsettled.  Leaf indices
+// stay below 2^21 (checked at upload).
+constexpr uint32_t LEAF_BITS = 21;
+constexpr uint32_t LEAF_MASK = (1u << LEAF_BITS) - 1;
+constexpr uint32_t TIE_SHIFT = LEAF_BITS;
+constexpr uint32_t TIE_MASK = 0x7Fu << TIE_SHIFT;
 
 struct alignas(16) DBvh {  // 64 B
     float xs[4];  // left.min.x, left.max.x, right.min.x, right.max.x
@@ -218,6 +226,9 @@ struct DevScene {
     // the rectangle at all (see ref_reaches_rect).
     const uint32_t* rect_anc;
     const float* abox;
+    // per rectangle, its innermost 4 list levels: start | width << 8 | boxes
+    // below (of rect_anc) << 16 | valid << 31 (tie_unsettled)
+    const uint32_t* rect_lvl;
     // Tie keys (general scenes): per sphere / rectangle / medium leaf, the
     // order in which the reference settles an exact tie in t (see
     // assignTieKeys in rtow_device.hip): the larger key wins.

@@ -6,7 +6,11 @@ BvhNode).  The reference asks the BvhNode with (tmin, t*) (hitableList.h:24-34)
 and AABB::hit returns `tmax <= tmin` (aabb.h:22-43), so the wall keeps the
 record; a third Box, in a BvhNode whose box starts before the plane, takes the
 tie (closed rectangle interval, xy_rect.h).  CPU: the oracle reproduces the
-reference bit for bit."""
+reference bit for bit.  GPU: the culled traversal settles the tie by the tie
+keys and marks it (the tie bits of the record); tie_unsettled finds the
+Boxes' BvhNode entered at the tied t below the list where the paths part, and
+the ray is settled by xhit, the reference's own recursion: the frame within
+the bar (without that: 8 % of the pixels differed, RMS up to 3e-2)."""
 import ctypes
 import json
 import os
@@ -51,9 +55,7 @@ def test_fixture_holds_the_culled_tie():
 
 @pytest.mark.gpu
 def test_gpu_matches_reference(gpu_ctx):
-    """The device settles the tie as the reference does (rect_reaches_tie:
-    the BvhNode boxes between the list and the rectangle, asked with the
-    list's closest hit so far): within the north-star bar, segment count equal."""
+    """Within the north-star bar, segment count equal."""
     import rtow
 
     c, d, ocam, op = setup()
