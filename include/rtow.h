@@ -190,9 +190,9 @@ typedef struct rtow_params {
     uint32_t samples_per_chunk; /* work granularity: a work item is one pixel's chunk of consecutive
                                     samples, summed in float in sample order (main.cpp:946) and added to
                                     the pixel's sum in 192-bit fixed point (order-independent, exact);
-                                    0 = auto (64, 32 or 16: the longest leaving >= 64 items per lane of
-                                    the grid, or spp/200 if larger; the last spc..2spc samples cut into
-                                    halving chunks) */
+                                    0 = auto (128, 64, 32 or 16: the longest leaving >= 60 items per
+                                    lane of the grid, or spp/200 if larger; the last spc..2spc samples
+                                    cut into halving chunks) */
     uint64_t seed;              /* render stream seed (rtow_rng.h) */
     uint32_t rank, world;       /* tile partition; world 0 is treated as 1 */
     uint32_t flags;

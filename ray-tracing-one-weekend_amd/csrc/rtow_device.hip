@@ -128,6 +128,8 @@ struct DevParams {
     // the DBG kernel records (RTOW_DEBUG_SEG_FLOATS floats each) into dbg_out
     uint32_t dbg_col, dbg_row, dbg_sample, dbg_max;
     float* dbg_out;
+    struct XFrame* xframes;  // xhit's call frames: XDEPTH x xstride (the grid's threads)
+    uint32_t xstride;
 };
 
 struct Rec {
@@ -645,6 +647,10 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
         if (sph_root(c, b0.w, r, a, ra, tmin, t)) take_hit(S, t, bt, best, refb);
     } else {
         hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) != DK_NONE;
+        if (hb && (refb >> KIND_SHIFT) == DK_BOX6) {  // a Box leaf: its sides right here, no visit of its own
+            box6_scan(S, refb & INDEX_MASK, r, q.inv, tmin, bt, best);
+            hb = false;
+        }
     }
     if ((refa >> KIND_SHIFT) == DK_SPHERE) {
         const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
@@ -652,6 +658,10 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
         if (sph_root(c, a0.w, r, a, ra, tmin, t)) take_hit(S, t, bt, best, refa);
     } else {
         ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) != DK_NONE;
+        if (ha && (refa >> KIND_SHIFT) == DK_BOX6) {
+            box6_scan(S, refa & INDEX_MASK, r, q.inv, tmin, bt, best);
+            ha = false;
+        }
     }
     if (ha && hb) {
         const bool afirst = ta <= tb;
@@ -1342,9 +1352,14 @@ __device__ __forceinline__ bool xrect(const XHit& H, const Ray& r, float t0, flo
 // The closest hit of the world for ray `wr` (world frame) in (tmin, FLT_MAX),
 // as color.h:17 asks for it; false: nothing hit (or the frames ran out:
 // `overflow`).
-__device__ __forceinline__ bool xhit(const DevScene& S, const Ray& wr, float tmin, Rng& rng, Rec& out,
+// The frames live in global memory (DevParams::xframes: frame k of grid
+// thread i at [k * xstride + i]), not in private scratch: a per-lane scratch
+// array of 4.6 KB made the runtime size every wave's scratch for it and cost
+// the general kernels 8-12 % although xhit itself runs for rare rays.
+__device__ __forceinline__ bool xhit(const DevScene& S, const DevParams& P, const Ray& wr, float tmin, Rng& rng, Rec& out,
                                      uint32_t& overflow) {
-    XFrame fr[XDEPTH];
+    XFrame* const fr0 = P.xframes + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t fs = P.xstride;
     int d = 0;
     bool rh = false;  // the result a finished call hands its caller
     Rec rr;
@@ -1357,7 +1372,7 @@ __device__ __forceinline__ bool xhit(const DevScene& S, const Ray& wr, float tmi
             rh = false;
             return;
         }
-        XFrame& F = fr[d++];
+        XFrame& F = fr0[fs * (size_t)d++];
         F.h = h;
         F.phase = 0;
         F.tmin = t0;
@@ -1366,7 +1381,7 @@ __device__ __forceinline__ bool xhit(const DevScene& S, const Ray& wr, float tmi
     };
     call(S.xroot, wr, tmin, FLT_MAX);
     while (d > 0) {
-        XFrame& F = fr[d - 1];
+        XFrame& F = fr0[fs * (size_t)(d - 1)];
         const XHit& H = S.xh[F.h];
         const uint32_t ph = F.phase;
         switch (H.kind) {
@@ -1966,7 +1981,7 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
 // words: the path state the traversal does not read, parked while it runs
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
-constexpr int COLD = 12;
+constexpr int COLD = 15;
 
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
@@ -2002,8 +2017,14 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     uint32_t* cold = reinterpret_cast<uint32_t*>(smem + 5120 + (size_t)STACK * BS * 4) + threadIdx.x;  // general only
     const uint32_t lane = threadIdx.x & 63u;
 
-    uint32_t item = 0, lpx = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0, overflow = 0;
-    uint32_t fx_range = 0;
+    uint32_t item = 0, lpx = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0;
+    // the two error flags: registers in the simple kernel, LDS words (COLD
+    // slots 13 and 14) in the register-bound general kernels
+    uint32_t overflow_reg = 0, fx_range_reg = 0;
+    uint32_t& overflow = SIMPLE ? overflow_reg : cold[13 * BS];
+    uint32_t& fx_range = SIMPLE ? fx_range_reg : cold[14 * BS];
+    overflow = 0;
+    fx_range = 0;
     uint32_t nseg_dbg = 0;
     bool need_item = true, need_sample = false;
     F3 acc = f3(0, 0, 0), thr = f3(1, 1, 1);
@@ -2098,7 +2119,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 t_mark = t_now;
             }
         } else if constexpr (MODE == 6) {
-            hit = xhit(S, ray, 0.001f, rng, rec, overflow);
+            hit = xhit(S, P, ray, 0.001f, rng, rec, overflow);
         } else {
             // park the path state the traversal does not need (COLD)
             cold[0 * BS] = __float_as_uint(acc.x);
@@ -2115,7 +2136,7 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             cold[11 * BS] = depth;
             Best best;
             best.prim = 0;
-            const Rng rng0 = rng;
+            cold[12 * BS] = rng.ctr;  // the draw counter at the segment's start (an xhit re-trace restarts there)
             if constexpr (PROF) {
                 const unsigned long long t_now = __builtin_amdgcn_s_memtime();
                 prof.cyc_other += t_now - t_mark;
@@ -2136,8 +2157,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             if (hit && (best.prim >> KIND_SHIFT) == DK_RECT &&
                 (ref_skips_hit(S, best.prim & LEAF_MASK, ray, best.t, 0.001f) ||
                  tie_unsettled(S, best.prim, ray, 0.001f, best.t))) {
-                rng = rng0;
-                hit = xhit(S, ray, 0.001f, rng, rec, overflow);
+                rng.ctr = cold[12 * BS];  // same draws (the key is the sample's)
+                hit = xhit(S, P, ray, 0.001f, rng, rec, overflow);
             } else if (hit) {
                 finalize<false>(S, best.prim & ~TIE_MASK, best.t, ray, rec);
             }
@@ -3685,8 +3706,9 @@ void buildTop(HostLayout& L) {
 // The DNode twin of every DBvh of a general scene (DevScene::gnode): sphere
 // children with time0 = 0, time1 = 1 inline (center(time) = c0 + time * dc
 // exactly, as sph_center computes it for them), other children as box slots
-// (a non-inlined sphere as DK_MSPHERE); a lone sphere child goes to slot b,
-// as in sahBuild.
+// (a non-inlined sphere as DK_MSPHERE, a Box as DK_BOX6: dnode_step scans its
+// sides when its box is hit instead of visiting it); a lone sphere child goes
+// to slot b, as in sahBuild.
 void buildGeneralNodes(HostLayout& L) {
     L.node.assign(L.bvh.size(), DNode{});
     for (size_t i = 0; i < L.bvh.size(); i++) {
@@ -3704,6 +3726,8 @@ void buildGeneralNodes(HostLayout& L) {
                 const DSphere& sp = L.sph[refs[k] & INDEX_MASK];
                 inl[k] = sp.t0 == 0.0f && sp.t1 == 1.0f;
                 if (!inl[k]) refs[k] = mkref(DK_MSPHERE, refs[k] & INDEX_MASK);
+            } else if ((refs[k] >> KIND_SHIFT) == DK_RECTS && L.list[refs[k] & INDEX_MASK].box6) {
+                refs[k] = mkref(DK_BOX6, L.list[refs[k] & INDEX_MASK].box6 - 1);  // scanned in the node step
             }
         }
         if (inl[0] && !inl[1]) {
@@ -3971,6 +3995,8 @@ struct rtow_context {
     bool has_scene = false;
     // work buffers
     void* d_work = nullptr;  // [0] work counter (u32) | [8..] u64 counters
+    void* d_xframes = nullptr;  // xhit's call frames (general scenes)
+    size_t xframes_bytes = 0;
     unsigned long long* d_fx = nullptr;  // pixel sums of one render (fx_add): three limb planes, 96 B per local pixel
     size_t fx_bytes = 0;
     uint8_t* d_fb = nullptr;  // rtow_render: BGRA frame + linear frame
@@ -4027,8 +4053,15 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
     uint32_t grid = (uint32_t)c->cus * per;
     uint32_t maxUseful = (P.n_items + BS - 1) / BS;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
+    DevParams Pk = P;
+    if constexpr (MODE != 0) {  // xhit's call frames, one column per grid thread
+        Pk.xstride = grid * (uint32_t)BS;
+        const int rc = ensure((void**)&c->d_xframes, &c->xframes_bytes, (size_t)Pk.xstride * XDEPTH * sizeof(XFrame));
+        if (rc) return rc;
+        Pk.xframes = (XFrame*)c->d_xframes;
+    }
     hipLaunchKernelGGL((trace_kernel<MODE, STACK, WAVES, PROF, BS, LDSN, DBG>), dim3(grid), dim3(BS), lds, st, c->scene,
-                       cam, P,
+                       cam, Pk,
                        (uint32_t*)c->d_work, c->fx_cur, (unsigned long long*)((uint8_t*)c->d_work + 8));
     HIP_TRY(hipGetLastError());
     return RTOW_OK;
@@ -4089,10 +4122,12 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     P.height = p->height;
     P.spp = p->spp;
     // Automatic chunking: the longest items (fewer refills and pixel-sum
-    // atomics: 64 samples are 4.6 % faster than 16 on config 2) that still
-    // leave >= 64 items per lane of the grid (cus x 1024 lanes), so a rank's
+    // atomics: on config 2, 64 samples are 4.6 % faster than 16 and 128 another
+    // 0.4 %, with 3.6 instead of 16.6 GB of atomic write traffic) that still
+    // leave >= 60 items per lane of the grid (cus x 1024 lanes), so a rank's
     // share of a multi-GPU frame keeps a short tail (config 2 over 8 ranks:
-    // 16-sample items 0.927 of the ideal, 64-sample 0.877; tools/rank_share.py).
+    // 16-sample items 0.947 of the ideal, 64-sample 0.877; tools/rank_share.py):
+    // config 2 gets 128 on one GPU, 64 on two, 16 on eight.
     // RTOW_AUTO_SPC (c->auto_spc) fixes the length instead.
     const uint32_t n_px = rtow_rank_tile_count(p->width, p->height, p->rank, world) * 64u;
     uint32_t spc = p->samples_per_chunk;
@@ -4100,8 +4135,8 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     if (!spc) {
         const uint64_t lanes = (uint64_t)std::max(1, c->cus) * 1024u;
         spc = 16;
-        for (uint32_t cand : {64u, 32u}) {
-            if ((uint64_t)n_px * ((p->spp + cand - 1) / cand) >= 64 * lanes) {
+        for (uint32_t cand : {128u, 64u, 32u}) {
+            if ((uint64_t)n_px * ((p->spp + cand - 1) / cand) >= 60 * lanes) {
                 spc = cand;
                 break;
             }
@@ -4315,6 +4350,7 @@ int rtow_context_destroy(rtow_context* c) {
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_work) (void)hipFree(c->d_work);
     if (c->d_fx) (void)hipFree(c->d_fx);
+    if (c->d_xframes) (void)hipFree(c->d_xframes);
     if (c->d_fb) (void)hipFree(c->d_fb);
     if (c->d_accum) (void)hipFree(c->d_accum);
     for (auto& ev : c->ev)

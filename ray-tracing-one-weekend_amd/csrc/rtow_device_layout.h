@@ -36,6 +36,7 @@ enum : uint32_t {
     DK_RECTS = 11,     // a list of rectangles only (a Box's sides): DList over rect[first, first+count)
     DK_PROG = 12,      // a BvhNode subtree holding media, visited as the reference visits it (DProg)
     DK_PROGNEXT = 13,  // traversal-stack marker: continue a DProg program at prog[index]
+    DK_BOX6 = 14,      // a general DNode slot holding a Box (index into box6): its sides scanned in the node step
     DK_NONE = 15
 };
 

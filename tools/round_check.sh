@@ -1,11 +1,12 @@
 #!/bin/bash
 # One GPU call: the GPU test suite, smoke(), the bench kernel's profile and the
 # general configs' profiles (tools/profile_bench.sh TAG_<workload>), and every
-# BASELINE config at full size (tools/bench_configs.py).
-# GPU box, repo root: bash tools/round_check.sh TAG [steps: tests,profile,general,configs]
+# BASELINE config at full size (tools/bench_configs.py), whole-frame parity of
+# every config against the oracle (tools/validate.py).
+# GPU box, repo root: bash tools/round_check.sh TAG [steps: tests,profile,general,configs,validate]
 set -o pipefail
 TAG=${1:-r03}
-STEPS=${2:-tests,profile,general,configs}
+STEPS=${2:-tests,profile,general,configs,validate}
 R=$(pwd)
 mkdir -p gpurun_out
 if [[ $STEPS == *tests* ]]; then
@@ -27,5 +28,9 @@ fi
 if [[ $STEPS == *configs* ]]; then
   cd $R
   timeout -k 10 600 python tools/bench_configs.py --configs 1,2,3,4,5 --cpu-seconds 3 \
-      --out gpurun_out/configs_$TAG.jsonl > gpurun_out/configs_$TAG.log 2>&1
+      --out gpurun_out/configs_$TAG.jsonl > gpurun_out/configs_$TAG.log 2>&1 || exit $?
+fi
+if [[ $STEPS == *validate* ]]; then
+  cd $R
+  timeout -k 10 600 python tools/validate.py --out gpurun_out/validation_$TAG.jsonl > gpurun_out/validate_$TAG.log 2>&1 || exit $?
 fi
