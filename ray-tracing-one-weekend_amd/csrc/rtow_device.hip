@@ -602,6 +602,9 @@ __device__ __forceinline__ bool tie_unsettled(const DevScene& S, uint32_t prim, 
     const uint32_t info = (prim & TIE_MASK) >> TIE_SHIFT;
     if (!info) return false;
     const uint32_t p = info - 1u, rect = prim & LEAF_MASK;
+    // the common ties (Boxes' coplanar sides in one BVH) part at a BvhNode:
+    // rect_lmask marks the key bits of the list levels that have boxes below
+    if (!((S.rect_lmask[rect] << p) >> 63)) return false;
     const uint32_t a = S.rect_anc[rect], cnt = a & 255u, off = a >> 8;
     if (cnt == 0) return false;
     for (int k = 0; k < 4; k++) {
@@ -1981,7 +1984,7 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
 // words: the path state the traversal does not read, parked while it runs
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
-constexpr int COLD = 15;
+constexpr int COLD = 13;
 
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
@@ -2017,14 +2020,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     uint32_t* cold = reinterpret_cast<uint32_t*>(smem + 5120 + (size_t)STACK * BS * 4) + threadIdx.x;  // general only
     const uint32_t lane = threadIdx.x & 63u;
 
-    uint32_t item = 0, lpx = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0;
-    // the two error flags: registers in the simple kernel, LDS words (COLD
-    // slots 13 and 14) in the register-bound general kernels
-    uint32_t overflow_reg = 0, fx_range_reg = 0;
-    uint32_t& overflow = SIMPLE ? overflow_reg : cold[13 * BS];
-    uint32_t& fx_range = SIMPLE ? fx_range_reg : cold[14 * BS];
-    overflow = 0;
-    fx_range = 0;
+    uint32_t item = 0, lpx = 0, s = 0, s_end = 0, col = 0, row = 0, depth = 0, nseg = 0, overflow = 0;
+    uint32_t fx_range = 0;
     uint32_t nseg_dbg = 0;
     bool need_item = true, need_sample = false;
     F3 acc = f3(0, 0, 0), thr = f3(1, 1, 1);
@@ -2417,6 +2414,7 @@ struct HostLayout {
     std::vector<float> collapsed_own;
     std::unordered_map<uint32_t, uint32_t> collapsed_of;
     std::vector<uint32_t> rect_lvl;  // DevScene::rect_lvl
+    std::vector<unsigned long long> rect_lmask;  // DevScene::rect_lmask
     std::vector<uint32_t> rect_anc;  // DevScene::rect_anc
     std::vector<float> abox;         // DevScene::abox
     std::vector<DProg> prog;         // DevScene::prog
@@ -2627,7 +2625,14 @@ void assignTieKeys(HostLayout& L, uint32_t ref, std::vector<KeyComp>& path, TieW
             at += c.bits;
         }
         const size_t from = lv.size() > 4 ? lv.size() - 4 : 0;
-        for (size_t k = from; k < lv.size(); k++) L.rect_lvl[4 * (size_t)rect + (k - from)] = lv[k];
+        unsigned long long mask = 0;
+        for (size_t k = from; k < lv.size(); k++) {
+            L.rect_lvl[4 * (size_t)rect + (k - from)] = lv[k];
+            const uint32_t st = lv[k] & 255u, w = (lv[k] >> 8) & 255u;
+            if ((lv[k] >> 16) & 255u)
+                for (uint32_t b = st; b < st + w && b < 64; b++) mask |= 1ull << (63 - b);
+        }
+        L.rect_lmask[rect] = mask;
     };
     const bool collapsed = L.collapsed_of.count(ref) != 0;  // an n == 1 BvhNode's box (refAncestors)
     if (collapsed) tw.boxes++;
@@ -3874,6 +3879,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     L.rect_key.assign(L.rect.size(), 0ull);
     L.med_key.assign(L.med.size(), 0ull);
     L.rect_lvl.assign(4 * L.rect.size(), 0u);
+    L.rect_lmask.assign(L.rect.size(), 0ull);
     {
         std::vector<KeyComp> path;
         TieWalk tw;
@@ -4404,7 +4410,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     if (L.rect_anc.empty()) L.rect_anc.push_back(0u);
     if (L.abox.empty()) L.abox.assign(8, 0.0f);
     if (L.rect_lvl.size() < 4) L.rect_lvl.resize(4, 0u);
+    if (L.rect_lmask.empty()) L.rect_lmask.push_back(0ull);
     size_t o_anc = pushBlob(blob, L.rect_anc), o_abox = pushBlob(blob, L.abox), o_lvl = pushBlob(blob, L.rect_lvl);
+    size_t o_lmask = pushBlob(blob, L.rect_lmask);
     if (L.prog.empty()) L.prog.push_back(DProg{});
     size_t o_prog = pushBlob(blob, L.prog);
     if (L.box6.empty()) L.box6.push_back(DBox6{});
@@ -4446,6 +4454,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.rect_anc = (const uint32_t*)(b + o_anc);
     d.abox = (const float*)(b + o_abox);
     d.rect_lvl = (const uint32_t*)(b + o_lvl);
+    d.rect_lmask = (const unsigned long long*)(b + o_lmask);
     d.prog = (const DProg*)(b + o_prog);
     d.box6 = (const DBox6*)(b + o_box6);
     for (int a = 0; a < 3; a++) d.tshift[a] = L.tshift[a];

@@ -230,6 +230,7 @@ struct DevScene {
     // per rectangle, its innermost 4 list levels: start | width << 8 | boxes
     // below (of rect_anc) << 16 | valid << 31 (tie_unsettled)
     const uint32_t* rect_lvl;
+    const unsigned long long* rect_lmask;  // per rectangle: the key bits of those levels with boxes below
     // Tie keys (general scenes): per sphere / rectangle / medium leaf, the
     // order in which the reference settles an exact tie in t (see
     // assignTieKeys in rtow_device.hip): the larger key wins.
