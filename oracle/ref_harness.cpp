@@ -306,6 +306,40 @@ static Hitable* tieBvhEntryNed() {
     return new HitableList(list, 5);
 }
 
+// Residual corner (i): one exact primary ray (tests/golden/make_graze_golden.py
+// computes it with the oracle and writes the world's 14 parameters, C hex
+// floats, to the file $RTOW_GRAZE_PARAMS) grazes the edge of a Box held by an
+// n == 1 BvhNode: AABB::hit sees `tmax <= tmin` (aabb.h:22-43) and the Box's
+// sides are never tested, although the side's rectangle (closed bounds,
+// xy_rect.h) would take the edge point.  Behind it in the list a
+// ConstantMedium whose boundary the ray enters beyond that point, then a
+// sphere in front of both: the reference asks the medium with the whole
+// interval and draws its scatter distance; a traversal that took the grazed
+// side would hand the medium that side's t, skip the draw, and end at the
+// same sphere with the stream one draw behind.
+static Hitable* grazeMediumNed() {
+    const char* path = std::getenv("RTOW_GRAZE_PARAMS");
+    float q[14] = {};
+    FILE* f = path ? std::fopen(path, "r") : nullptr;
+    if (!f) { std::fprintf(stderr, "RTOW_GRAZE_PARAMS not readable\n"); std::exit(2); }
+    for (int k = 0; k < 14; k++) {
+        char buf[64];
+        if (std::fscanf(f, "%63s", buf) != 1) { std::fprintf(stderr, "short graze params\n"); std::exit(2); }
+        q[k] = std::strtof(buf, nullptr);
+    }
+    std::fclose(f);
+    Material* blue = new Lambertian(new ConstantTexture(vec3(0.1, 0.2, 0.8)));
+    Hitable** box = new Hitable*[1];
+    box[0] = new Box(vec3(q[0], q[1], q[2]), vec3(q[3], q[4], q[5]), blue);
+    Hitable** list = new Hitable*[4];
+    list[0] = new BvhNode(box, 1, 0.0f, 1.0f);
+    list[1] = new ConstantMedium(new Sphere(vec3(q[6], q[7], q[8]), q[9], new Dielectric(1.5)), 0.4f,
+                                 new ConstantTexture(vec3(0.9, 0.9, 0.9)));
+    list[2] = new Sphere(vec3(q[10], q[11], q[12]), q[13], new Lambertian(new ConstantTexture(vec3(0.8, 0.3, 0.2))));
+    list[3] = new Sphere(vec3(q[0], q[1], q[2] - 40), 10, new DiffuseLight(new ConstantTexture(vec3(3, 3, 3))));
+    return new HitableList(list, 4);
+}
+
 // Config 4: cornellBox_NED() with the smoke box that scenes.h:461-470 keeps
 // commented out, inserted at the position that code occupies (after the
 // rotated box, before the sphere medium).
@@ -410,6 +444,7 @@ static Hitable* buildWorld(const std::string& name, const Opts& o) {
     if (name == "medium_bvh") return mediumBvhNed();
     if (name == "medium_nested") return mediumNestedNed();
     if (name == "tie_bvh_entry") return tieBvhEntryNed();
+    if (name == "graze_medium") return grazeMediumNed();
     if (name == "medium_bvh_wrapped") return mediumBvhWrappedNed();
     if (name == "final_ned") {
         bool used;

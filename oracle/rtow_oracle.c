@@ -544,13 +544,11 @@ static v3 color(ctx_t* cx, rng_t* g, const rtow_params* P, const ray_t* r, int d
 }
 
 /* ---- render loop (main.cpp:932-996 + camera.h:123-135) ------------------- */
-static v3 sample_color(ctx_t* cx, const rtow_camera* C, const rtow_params* P, int column, int row, uint32_t s) {
+/* main.cpp:942-944 + Camera::getRay (camera.h:123-135): the sample's primary ray */
+static ray_t camera_ray(ctx_t* cx, rng_t* gp, const rtow_camera* C, const rtow_params* P, int column, int row) {
     const uint32_t W = P->width, H = P->height;
+    rng_t g = *gp;
     {
-        rng_t g;
-        g.key = rtow_sample_key(P->seed, (uint32_t)row * W + (uint32_t)column, s);
-        g.ctr = 0;
-        uint64_t d0 = cx->c.draws;
         float u = (float)(column + unif(cx, &g)) / (float)W;
         float v = (float)(row + unif(cx, &g)) / (float)H;
         /* camera.h:123-135: CAMERA_DOF_EN 0 (the reference default) or, with
@@ -575,11 +573,23 @@ static v3 sample_color(ctx_t* cx, const rtow_camera* C, const rtow_params* P, in
                       ld3(C->origin)),
                   offset);
         r.time = time;
+        *gp = g;
+        return r;
+    }
+}
+
+static v3 sample_color(ctx_t* cx, const rtow_camera* C, const rtow_params* P, int column, int row, uint32_t s) {
+    const uint32_t W = P->width;
+    {
+        rng_t g;
+        g.key = rtow_sample_key(P->seed, (uint32_t)row * W + (uint32_t)column, s);
+        g.ctr = 0;
+        uint64_t d0 = cx->c.draws;
+        ray_t r = camera_ray(cx, &g, C, P, column, row);
         v3 c = color(cx, &g, P, &r, 0);
         cx->c.samples++;
         uint64_t nd = cx->c.draws - d0;
         if (nd > cx->c.max_draws_per_sample) cx->c.max_draws_per_sample = nd;
-        (void)H;
         return c;
     }
 }
@@ -766,4 +776,23 @@ void rtow_oracle_free(rtow_oracle_scene* s) {
     if (!s) return;
     free(s->blob);
     free(s);
+}
+
+/* The primary ray of one sample (column, row in the reference's numbering:
+ * row 0 = the bottom image row), as the render loop computes it: origin xyz,
+ * direction xyz, time.  Test infrastructure (tests/golden/make_graze_golden.py
+ * builds a world around one exact ray). */
+int rtow_oracle_camera_ray(const rtow_camera* cam, const rtow_params* p, uint32_t column, uint32_t row,
+                           uint32_t sample, float* out7) {
+    if (!cam || !p || !out7 || column >= p->width || row >= p->height) return RTOW_E_INVALID;
+    ctx_t cx;
+    memset(&cx, 0, sizeof cx);
+    rng_t g;
+    g.key = rtow_sample_key(p->seed, row * p->width + column, sample);
+    g.ctr = 0;
+    ray_t r = camera_ray(&cx, &g, cam, p, (int)column, (int)row);
+    out7[0] = r.o.x, out7[1] = r.o.y, out7[2] = r.o.z;
+    out7[3] = r.d.x, out7[4] = r.d.y, out7[5] = r.d.z;
+    out7[6] = r.time;
+    return 0;
 }

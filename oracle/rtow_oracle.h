@@ -57,6 +57,9 @@ int rtow_oracle_render_pixels(const rtow_scene* scene, const rtow_camera* cam, c
 /* Whole frame, framebuffer order: lin W*H*3, bgra W*H*4 (either may be NULL). */
 int rtow_oracle_render(const rtow_scene* scene, const rtow_camera* cam, const rtow_params* p,
                        int threads, float* lin, uint8_t* bgra, rtow_oracle_counters* counters);
+/* The primary ray of one sample: origin xyz, direction xyz, time. */
+int rtow_oracle_camera_ray(const rtow_camera* cam, const rtow_params* p, uint32_t column, uint32_t row,
+                           uint32_t sample, float* out7);
 
 /* The path of one sample (pixel x, y of the top-down frame): per color() call
  * RTOW_DEBUG_SEG_FLOATS floats, the records rtow_debug_trace_sample writes. */

@@ -1142,6 +1142,9 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                 // asked with the closest hit so far, or (tmed, set by a DProg
                 // program) its subtree's interval; the nearest record is kept
                 float tm = tmed == tmed ? tmed : bt;
+                if (!(tmed == tmed) && (best.prim >> KIND_SHIFT) == DK_RECT &&
+                    ref_skips_hit(S, best.prim & LEAF_MASK, wray, bt, tmin))
+                    overflow |= 2u;  // see traverse_top's TOP_MEDIUM
                 tmed = __builtin_nanf("");
                 if (medium_hit<STACK, ANYB>(S, idx, r, a, wray, tmin, tm, stk, sp, rng, overflow) &&
                     take_hit(S, tm, bt, best.prim, cur))
@@ -1223,7 +1226,11 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             }
         } else if (TOPMED && T.kind == TOP_MEDIUM) {
             // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
-            // so far as tmax, in the medium's frame; it draws as the reference
+            // so far as tmax, in the medium's frame; it draws as the reference.
+            // A record the reference never reached (a rectangle grazed at its
+            // box's edge, ref_skips_hit) would cut the medium's interval and
+            // maybe its draws: the ray is then settled by xhit (overflow bit 1)
+            if ((bp >> KIND_SHIFT) == DK_RECT && ref_skips_hit(S, bp & LEAF_MASK, wray, bt, tmin)) overflow |= 2u;
             if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) {
                 bp = mkref(DK_MEDIUM, T.a);
                 found = true;
@@ -2151,9 +2158,11 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             // the t of a tie it won (tie_unsettled) -- and the record is the
             // reference's only by its own recursion: the ray again, same
             // draws, through xhit (the exact-order kernel's hit()).
-            if (hit && (best.prim >> KIND_SHIFT) == DK_RECT &&
-                (ref_skips_hit(S, best.prim & LEAF_MASK, ray, best.t, 0.001f) ||
-                 tie_unsettled(S, best.prim, ray, 0.001f, best.t))) {
+            // (also a medium whose interval such a rectangle cut: overflow bit 1)
+            if ((overflow & 2u) || (hit && (best.prim >> KIND_SHIFT) == DK_RECT &&
+                                    (ref_skips_hit(S, best.prim & LEAF_MASK, ray, best.t, 0.001f) ||
+                                     tie_unsettled(S, best.prim, ray, 0.001f, best.t)))) {
+                overflow &= 1u;
                 rng.ctr = cold[12 * BS];  // same draws (the key is the sample's)
                 hit = xhit(S, P, ray, 0.001f, rng, rec, overflow);
             } else if (hit) {

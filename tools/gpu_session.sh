@@ -2,6 +2,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > gpurun_out/gputests_r03f.log 2>&1
-AB_SCENES=cornell_smoke,final_ned,cornell AB_SPP=256 AB_ROUNDS=2 timeout -k 10 300 python tools/ab.py ab/nobvh.so ab/gf.so ab/box.so ab/flags.so > gpurun_out/ab_gf.log 2>&1 || exit $?
-AB_SCENES=random_ned AB_SPP=1024 AB_ROUNDS=2 AB_SPC=0 timeout -k 10 300 python tools/ab.py ab/nobvh.so ray-tracing-one-weekend_amd/librtow_hip.so > gpurun_out/ab_rn.log 2>&1 || exit $?
+AB_SCENES=final_ned,cornell_smoke AB_SPP=256 AB_ROUNDS=2 timeout -k 10 300 python tools/ab.py ab/nobvh.so ab/box.so ab/lmask.so > gpurun_out/ab_lmask.log 2>&1 || exit $?
+bash tools/round_check.sh r03 > gpurun_out/round_check_r03.log 2>&1
