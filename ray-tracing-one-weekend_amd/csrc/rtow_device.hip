@@ -501,6 +501,17 @@ __device__ __forceinline__ bool ref_skips_hit(const DevScene& S, uint32_t rect, 
     const bool edge = x - q.a0 < ex || q.a1 - x < ex || y - q.b0 < ey || q.b1 - y < ey;
     return edge && !ref_reaches_rect(S, rect, r, tmin);
 }
+// ref_skips_hit for a rectangle hit at the t its plane gives (rect_t's
+// division: the t it held the record at)
+__device__ __forceinline__ bool ref_skips_rect(const DevScene& S, uint32_t rect, const Ray& wray, float tmin) {
+    if ((S.rect_anc[rect] & 255u) == 0) return false;
+    const DRect q = S.rect[rect];
+    const Ray r = chain_ray(S, q.chain, wray);
+    uint32_t i, j, k;
+    rect_axes(q.axis & 3u, i, j, k);
+    const float dk = comp(r.d, k);
+    return ref_skips_hit(S, rect, wray, div_by_any(q.k - comp(r.o, k), dk, 1.0f / dk), tmin);
+}
 
 // A Box's six sides (DBox6) in their list order (box.h:29-38), each tested as
 // the rectangle-list loop tests it: the interval [tmin, bt] shrinks as sides
@@ -650,10 +661,6 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
         if (sph_root(c, b0.w, r, a, ra, tmin, t)) take_hit(S, t, bt, best, refb);
     } else {
         hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) != DK_NONE;
-        if (hb && (refb >> KIND_SHIFT) == DK_BOX6) {  // a Box leaf: its sides right here, no visit of its own
-            box6_scan(S, refb & INDEX_MASK, r, q.inv, tmin, bt, best);
-            hb = false;
-        }
     }
     if ((refa >> KIND_SHIFT) == DK_SPHERE) {
         const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
@@ -661,10 +668,18 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
         if (sph_root(c, a0.w, r, a, ra, tmin, t)) take_hit(S, t, bt, best, refa);
     } else {
         ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) != DK_NONE;
-        if (ha && (refa >> KIND_SHIFT) == DK_BOX6) {
-            box6_scan(S, refa & INDEX_MASK, r, q.inv, tmin, bt, best);
-            ha = false;
-        }
+    }
+    // Box leaves: their sides right here, no visit of their own (one copy of
+    // the body for both slots; the order does not matter, ties go by the keys)
+    uint32_t l0 = hb && (refb >> KIND_SHIFT) == DK_BOX6 ? refb : 0u;
+    uint32_t l1 = ha && (refa >> KIND_SHIFT) == DK_BOX6 ? refa : 0u;
+    if (l0) hb = false;
+    if (l1) ha = false;
+    if (!l0) l0 = l1, l1 = 0u;
+    while (l0) {
+        box6_scan(S, l0 & INDEX_MASK, r, q.inv, tmin, bt, best);
+        l0 = l1;
+        l1 = 0u;
     }
     if (ha && hb) {
         const bool afirst = ta <= tb;
@@ -1169,6 +1184,9 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
                              uint32_t& overflow, Prof* prof = nullptr) {
     float bt = FLT_MAX;
     uint32_t bp = mkref(DK_NONE, 0);
+    // COLD slot 13 (the lane's LDS column past its stack): mrect, below
+    uint32_t* const mslot = stk + (size_t)(STACK + 13) * BLOCK;
+    if constexpr (TOPMED) *mslot = mkref(DK_NONE, 0);
     bool found = false;
     // per-direction constants, recomputed only when a chain turns the ray
     bool have = false;
@@ -1230,7 +1248,13 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             // A record the reference never reached (a rectangle grazed at its
             // box's edge, ref_skips_hit) would cut the medium's interval and
             // maybe its draws: the ray is then settled by xhit (overflow bit 1)
-            if ((bp >> KIND_SHIFT) == DK_RECT && ref_skips_hit(S, bp & LEAF_MASK, wray, bt, tmin)) overflow |= 2u;
+            // (checked after the scan, once: mrect, the rectangle holding the
+            // record when a medium was asked; a second one forces the re-trace)
+            if ((bp >> KIND_SHIFT) == DK_RECT) {
+                const uint32_t mrect = *mslot;
+                if ((mrect >> KIND_SHIFT) == DK_RECT && ((mrect ^ bp) & ~TIE_MASK)) overflow |= 2u;
+                *mslot = bp;
+            }
             if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) {
                 bp = mkref(DK_MEDIUM, T.a);
                 found = true;
@@ -1246,6 +1270,14 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
     }
     if constexpr (PROF) {
         if (n <= 8) prof->cyc_item[n - 1] += __builtin_amdgcn_s_memtime() - t0;
+    }
+    // a rectangle that cut a medium's interval and lost the record later (the
+    // winner itself is checked by the caller)
+    if constexpr (TOPMED) {
+        const uint32_t mrect = *mslot;
+        if ((mrect >> KIND_SHIFT) == DK_RECT && ((mrect ^ bp) & ~TIE_MASK) &&
+            ref_skips_rect(S, mrect & LEAF_MASK, wray, tmin))
+            overflow |= 2u;
     }
     best.t = bt;
     best.prim = bp;
@@ -1991,7 +2023,7 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
 // words: the path state the traversal does not read, parked while it runs
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
-constexpr int COLD = 13;
+constexpr int COLD = 14;
 
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
