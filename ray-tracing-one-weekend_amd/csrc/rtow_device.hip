@@ -1188,12 +1188,10 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
     uint32_t* const mslot = stk + (size_t)(STACK + 13) * BLOCK;
     if constexpr (TOPMED) *mslot = mkref(DK_NONE, 0);
     bool found = false;
-    // per-direction constants, recomputed only when a chain turns the ray
-    bool have = false;
-    uint32_t dx = 0, dy = 0, dz = 0;
+    // the ray in the item's frame and its per-direction constants, recomputed
+    // only where the host marked the item (TOP_NEWCHAIN / TOP_NEWDIR)
     F3 inv = f3(0, 0, 0);
     float a = 0, ra = 0;
-    uint32_t last_chain = ~0u;  // the chain `r` was computed for
     Ray r = wray;
     const uint32_t n = S.n_top ? S.n_top : 1u;  // no top-level list: the whole graph is one item
     unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
@@ -1205,7 +1203,8 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             t0 = t1;
         }
         const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
-        if (T.kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
+        const uint32_t kind = T.kind & TOP_KIND_MASK;
+        if (kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
             Best b;
             if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp,
                                              PROF ? prof : nullptr)) {
@@ -1216,15 +1215,11 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             continue;
         }
         unsigned long long tc = PROF ? __builtin_amdgcn_s_memtime() : 0;
-        // consecutive items in one frame (a room's walls) share the ray
-        if (T.chain != last_chain) {
-            last_chain = T.chain;
+        // consecutive items in one frame (a room's walls) share the ray, and
+        // frames that differ by translations only its direction constants
+        if (T.kind & TOP_NEWCHAIN) {
             r = chain_ray(S, T.chain, wray);
-            if (!have || __float_as_uint(r.d.x) != dx || __float_as_uint(r.d.y) != dy || __float_as_uint(r.d.z) != dz) {
-                have = true;
-                dx = __float_as_uint(r.d.x);
-                dy = __float_as_uint(r.d.y);
-                dz = __float_as_uint(r.d.z);
+            if (T.kind & TOP_NEWDIR) {
                 inv = inv_dir(r.d);
                 a = dot(r.d, r.d);
                 ra = 1.0f / a;
@@ -1234,15 +1229,15 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             __builtin_amdgcn_s_waitcnt(0);
             prof->cyc_chain += __builtin_amdgcn_s_memtime() - tc;
         }
-        if (T.kind == TOP_BOX6) {
+        if (kind == TOP_BOX6) {
             if (box6_scan(S, T.a, r, inv, tmin, bt, bp)) found = true;
-        } else if (T.kind == TOP_RECTS) {
+        } else if (kind == TOP_RECTS) {
             for (uint32_t k = 0; k < T.b; k++) {
                 float t;
                 if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t) && take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k)))
                     found = true;
             }
-        } else if (TOPMED && T.kind == TOP_MEDIUM) {
+        } else if (TOPMED && kind == TOP_MEDIUM) {
             // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
             // so far as tmax, in the medium's frame; it draws as the reference.
             // A record the reference never reached (a rectangle grazed at its
@@ -1259,9 +1254,9 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
                 bp = mkref(DK_MEDIUM, T.a);
                 found = true;
             }
-        } else if (T.kind == TOP_SPHERES) {
+        } else if (kind == TOP_SPHERES) {
             if (trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow)) found = true;
-        } else if (T.kind == TOP_SPHERE) {
+        } else if (kind == TOP_SPHERE) {
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
             float t;
@@ -3747,6 +3742,33 @@ void buildTop(HostLayout& L) {
         }
         L.top.push_back(t);
     }
+    // where the scan's ray changes (traverse_top): a new frame, and a new
+    // direction when the frames' rotations (their RotateY sines and cosines,
+    // in chain order: translations leave the direction alone) differ.  Items
+    // the general traversal runs (TOP_GENERIC) do not use the scan's ray.
+    auto dirSig = [&](uint32_t c) {
+        std::vector<uint64_t> v;
+        const DChain& C = L.chains[c];
+        for (uint32_t k = 0; k < C.n; k++) {
+            if ((C.ref[k] >> KIND_SHIFT) != DK_ROTY) continue;
+            const DInst& I = L.inst[C.ref[k] & INDEX_MASK];
+            uint32_t sb, cb;
+            std::memcpy(&sb, &I.p[0], 4);
+            std::memcpy(&cb, &I.p[1], 4);
+            v.push_back((uint64_t)sb << 32 | cb);
+        }
+        return v;
+    };
+    uint32_t last = ~0u;
+    std::vector<uint64_t> lastSig;
+    for (DTop& t : L.top) {
+        if (t.kind == TOP_GENERIC || t.chain == last) continue;
+        std::vector<uint64_t> sig = dirSig(t.chain);
+        t.kind |= TOP_NEWCHAIN;
+        if (last == ~0u || sig != lastSig) t.kind |= TOP_NEWDIR;
+        last = t.chain;
+        lastSig = std::move(sig);
+    }
 }
 
 // The DNode twin of every DBvh of a general scene (DevScene::gnode): sphere
@@ -4002,7 +4024,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     {
         std::vector<bool> top_med(L.med.size(), false);
         for (const DTop& t : L.top)
-            if (t.kind == TOP_MEDIUM) top_med[t.a] = true;
+            if ((t.kind & TOP_KIND_MASK) == TOP_MEDIUM) top_med[t.a] = true;
         for (size_t i = 0; i < L.med.size(); i++)
             if (!top_med[i]) L.media_nested = true;
     }

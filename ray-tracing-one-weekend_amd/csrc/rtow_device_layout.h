@@ -181,6 +181,10 @@ struct alignas(16) DProg {  // 32 B; lo/hi read as ref_aabb_hit's (min xyz, -, m
 // 1000 spheres))): TOP_SPHERES runs its DNode tree in a loop of its own
 // (trace_dnodes) in the leaves' frame, entered once per ray.
 enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2, TOP_MEDIUM = 3, TOP_BOX6 = 4, TOP_SPHERES = 5 };
+// DTop::kind flags above the kind (buildTop): the item's frame differs from
+// the previous in-place item's (the scan recomputes its ray), and so does the
+// ray's direction there (it recomputes 1/d and dot(d, d) too)
+enum : uint32_t { TOP_KIND_MASK = 255u, TOP_NEWCHAIN = 1u << 8, TOP_NEWDIR = 1u << 9 };
 // BOX6: a = box6 index; SPHERES: a = the DNode index of the BvhNode
 struct alignas(16) DTop {  // 16 B
     uint32_t kind;
