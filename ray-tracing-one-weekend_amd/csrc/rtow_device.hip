@@ -1187,7 +1187,6 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
     // COLD slot 13 (the lane's LDS column past its stack): mrect, below
     uint32_t* const mslot = stk + (size_t)(STACK + 13) * BLOCK;
     if constexpr (TOPMED) *mslot = mkref(DK_NONE, 0);
-    bool found = false;
     // the ray in the item's frame and its per-direction constants, recomputed
     // only where the host marked the item (TOP_NEWCHAIN / TOP_NEWDIR)
     F3 inv = f3(0, 0, 0);
@@ -1205,12 +1204,16 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
         const uint32_t kind = T.kind & TOP_KIND_MASK;
         if (kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
+            // the scan's ray is dead across the general traversal (the host
+            // marks the next in-place item to recompute it): registers
+            r = wray;
+            inv = f3(0, 0, 0);
+            a = ra = 0.0f;
             Best b;
             if (traverse<MEDIA, STACK, ANYB>(S, T.a, wray, T.chain, tmin, bt, stk, 0, rng, b, overflow, bp,
                                              PROF ? prof : nullptr)) {
                 bt = b.t;
                 bp = b.prim;
-                found = true;
             }
             continue;
         }
@@ -1230,12 +1233,11 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             prof->cyc_chain += __builtin_amdgcn_s_memtime() - tc;
         }
         if (kind == TOP_BOX6) {
-            if (box6_scan(S, T.a, r, inv, tmin, bt, bp)) found = true;
+            box6_scan(S, T.a, r, inv, tmin, bt, bp);
         } else if (kind == TOP_RECTS) {
             for (uint32_t k = 0; k < T.b; k++) {
                 float t;
-                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t) && take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k)))
-                    found = true;
+                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t)) take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k));
             }
         } else if (TOPMED && kind == TOP_MEDIUM) {
             // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
@@ -1250,17 +1252,14 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
                 if ((mrect >> KIND_SHIFT) == DK_RECT && ((mrect ^ bp) & ~TIE_MASK)) overflow |= 2u;
                 *mslot = bp;
             }
-            if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) {
-                bp = mkref(DK_MEDIUM, T.a);
-                found = true;
-            }
+            if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) bp = mkref(DK_MEDIUM, T.a);
         } else if (kind == TOP_SPHERES) {
-            if (trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow)) found = true;
+            trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
         } else if (kind == TOP_SPHERE) {
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
             float t;
-            if (sph_root(c, sp.r, r, a, ra, tmin, t) && take_hit(S, t, bt, bp, mkref(DK_SPHERE, T.a))) found = true;
+            if (sph_root(c, sp.r, r, a, ra, tmin, t)) take_hit(S, t, bt, bp, mkref(DK_SPHERE, T.a));
         }
     }
     if constexpr (PROF) {
@@ -1276,7 +1275,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
     }
     best.t = bt;
     best.prim = bp;
-    return found;
+    return (bp >> KIND_SHIFT) != DK_NONE;  // a record was taken
 }
 
 // x / d in double from r = RN(1/d): q0 = x*r, one fma residual step.  For the
@@ -3745,7 +3744,8 @@ void buildTop(HostLayout& L) {
     // where the scan's ray changes (traverse_top): a new frame, and a new
     // direction when the frames' rotations (their RotateY sines and cosines,
     // in chain order: translations leave the direction alone) differ.  Items
-    // the general traversal runs (TOP_GENERIC) do not use the scan's ray.
+    // the general traversal runs (TOP_GENERIC) do not use the scan's ray, and
+    // the first in-place item after one recomputes it.
     auto dirSig = [&](uint32_t c) {
         std::vector<uint64_t> v;
         const DChain& C = L.chains[c];
@@ -3762,7 +3762,11 @@ void buildTop(HostLayout& L) {
     uint32_t last = ~0u;
     std::vector<uint64_t> lastSig;
     for (DTop& t : L.top) {
-        if (t.kind == TOP_GENERIC || t.chain == last) continue;
+        if (t.kind == TOP_GENERIC) {  // (the kernel drops the scan's ray there)
+            last = ~0u;
+            continue;
+        }
+        if (t.chain == last) continue;
         std::vector<uint64_t> sig = dirSig(t.chain);
         t.kind |= TOP_NEWCHAIN;
         if (last == ~0u || sig != lastSig) t.kind |= TOP_NEWDIR;
