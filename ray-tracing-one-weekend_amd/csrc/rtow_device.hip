@@ -1179,7 +1179,9 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
 // hit so far.  The loop is uniform across the wave (see DTop).
 // MEDIA / ANYB: media below the top level (the general traversal asks them);
 // TOPMED: media as top-level items (TOP_MEDIUM).
-template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false>
+// PARK: the caller parked the sample's RNG key (COLD words 14, 15) and its
+// counter (16) in LDS; media draw through them (registers, see cold_words).
+template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false, bool PARK = false>
 __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
                              uint32_t& overflow, Prof* prof = nullptr) {
     float bt = FLT_MAX;
@@ -1252,7 +1254,16 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
                 if ((mrect >> KIND_SHIFT) == DK_RECT && ((mrect ^ bp) & ~TIE_MASK)) overflow |= 2u;
                 *mslot = bp;
             }
-            if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow)) bp = mkref(DK_MEDIUM, T.a);
+            if constexpr (PARK) {
+                uint32_t* const cw = stk + (size_t)STACK * BLOCK;
+                Rng m{(uint64_t)cw[15 * BLOCK] << 32 | cw[14 * BLOCK], cw[16 * BLOCK]};
+                if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, m, overflow))
+                    bp = mkref(DK_MEDIUM, T.a);
+                cw[16 * BLOCK] = m.ctr;
+            } else {
+                if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow))
+                    bp = mkref(DK_MEDIUM, T.a);
+            }
         } else if (kind == TOP_SPHERES) {
             trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
         } else if (kind == TOP_SPHERE) {
@@ -2017,11 +2028,15 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // (LDSN) the DNode array of a simple scene | (general scenes) COLD x BS
 // words: the path state the traversal does not read, parked while it runs
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
-constexpr int COLD = 14;
+// 14 words; 17 with a stack of 16 (MODE 5 parks the sample's RNG key and
+// counter there too, PARK_RNG): either way 4 blocks of 256 fit a CU's 160 KB.
+constexpr int cold_words(int STACK) { return STACK <= 16 ? 17 : 14; }
+template <int MODE, int STACK>
+constexpr bool park_rng() { return MODE == 5 && STACK <= 16; }
 
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
-           (general ? (size_t)COLD * BS * 4 : 0);
+           (general ? (size_t)cold_words(STACK) * BS * 4 : 0);
 }
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
@@ -2172,8 +2187,20 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 prof.cyc_other += t_now - t_mark;
                 t_mark = t_now;
             }
-            hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF>(S, ray, 0.001f, stk, rng, best,
-                                                                                       overflow, &prof);
+            constexpr bool PARK = park_rng<MODE, STACK>();
+            if constexpr (PARK) {  // the key and counter wait in LDS (media draw through them)
+                cold[14 * BS] = (uint32_t)rng.key;
+                cold[15 * BS] = (uint32_t)(rng.key >> 32);
+                cold[16 * BS] = rng.ctr;
+                rng.key = 0;
+                rng.ctr = 0;
+            }
+            hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF, PARK>(S, ray, 0.001f, stk, rng,
+                                                                                             best, overflow, &prof);
+            if constexpr (PARK) {
+                rng.key = (uint64_t)cold[15 * BS] << 32 | cold[14 * BS];
+                rng.ctr = cold[16 * BS];
+            }
             if constexpr (PROF) {
                 const unsigned long long t_now = __builtin_amdgcn_s_memtime();
                 prof.cyc_trav += t_now - t_mark;
@@ -4166,7 +4193,7 @@ int launchStack(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
     const uint32_t need = c->scene.stack_need;
     if (need <= 16) return launchWaves<MODE, 16>(c, cam, P, bpc, st);
     // general kernels: 20 entries keep 4 blocks of 256 per CU within LDS
-    // (tables + stack + COLD: 37 KB a block); final_ned needs 17
+    // (tables + stack + COLD: 39 KB a block)
     if constexpr (MODE != 0)
         if (need <= 20) return launchWaves<MODE, 20>(c, cam, P, bpc, st);
     if (need <= 32) return launchWaves<MODE, 32>(c, cam, P, bpc, st);
