@@ -563,6 +563,7 @@ struct Prof {
     unsigned long long cyc_trav, cyc_other;  // wave cycles (s_memtime) in traversal / everything else
     // general scenes: wave cycles per top-level item (first 8), in finalize, and the item visits
     unsigned long long cyc_item[8], cyc_fin, visits_item[8], cyc_chain;
+    uint32_t box_lanes, box_waves;  // Box leaf scans in node steps: lanes / wave executions
 };
 // General scenes: does leaf `cand`, hit at exactly the t of the current best
 // leaf `best`, take the record in the reference?  (assignTieKeys)
@@ -648,7 +649,7 @@ __device__ __forceinline__ bool first_active_lane() {
 template <int STACK>
 __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, const Ray& r, const SlabRay& q, float a,
                                                float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk, int& sp,
-                                               uint32_t& overflow) {
+                                               uint32_t& overflow, Prof* prof = nullptr) {
     const float4* np = reinterpret_cast<const float4*>(S.node + idx);
     const float4 a0 = np[0], a1 = np[1], b0 = np[2], b1 = np[3];
     const uint32_t refa = __float_as_uint(a1.w), refb = __float_as_uint(b1.w);
@@ -677,6 +678,10 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
     if (l1) ha = false;
     if (!l0) l0 = l1, l1 = 0u;
     while (l0) {
+        if (prof) {
+            prof->box_lanes++;
+            if (first_active_lane()) prof->box_waves++;
+        }
         box6_scan(S, l0 & INDEX_MASK, r, q.inv, tmin, bt, best);
         l0 = l1;
         l1 = 0u;
@@ -1036,7 +1041,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
         if (kind == DK_BVH) {
             const uint32_t before = best.prim;
             uint32_t b = before;
-            const uint32_t nxt = dnode_step<STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow);
+            const uint32_t nxt = dnode_step<STACK>(S, idx, r, q, a, ra, tmin, bt, b, stk, sp, overflow, prof);
             if (b != before) {
                 best.prim = b;
                 found = true;
@@ -1331,10 +1336,12 @@ __device__ __forceinline__ void finalize(const DevScene& S, uint32_t prim, float
         const DRect& q = S.rect[idx];
         uint32_t i, j, k;
         rect_axes(q.axis & 3u, i, j, k);
-        const float x = comp(r.o, i) + t * comp(r.d, i);
-        const float y = comp(r.o, j) + t * comp(r.d, j);
-        rec.u = (x - q.a0) / (q.a1 - q.a0);
-        rec.v = (y - q.b0) / (q.b1 - q.b0);
+        if (S.mat[q.mat].needs_uv) {  // (u, v reach nothing else: two divisions saved)
+            const float x = comp(r.o, i) + t * comp(r.d, i);
+            const float y = comp(r.o, j) + t * comp(r.d, j);
+            rec.u = (x - q.a0) / (q.a1 - q.a0);
+            rec.v = (y - q.b0) / (q.b1 - q.b0);
+        }
         rec.p = at(r, t);
         const float nv = (q.axis & RECT_FLIP) ? -1.0f : 1.0f;  // FlipNormals folded into the leaf
         const float zero = (q.axis & RECT_FLIP) ? -0.0f : 0.0f;
@@ -2311,6 +2318,15 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             }
             atomicAdd(&counters[32], prof.cyc_fin);
             atomicAdd(&counters[33], prof.cyc_chain);
+        }
+        {
+            uint32_t x = prof.box_lanes, y = prof.box_waves;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off), y += __shfl_xor(y, off);
+            if (lane == 0) {
+                atomicAdd(&counters[34], (unsigned long long)x);
+                atomicAdd(&counters[35], (unsigned long long)y);
+            }
         }
     }
 }
@@ -4368,6 +4384,9 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
         for (int k = 0; k < 8; k++)
             if (host_ctr[24 + k]) std::fprintf(stderr, " [%d] %.3f %llu", k, host_ctr[16 + k] / tot, host_ctr[24 + k]);
         std::fprintf(stderr, " | chain_ray+constants of in-place items %.3f\n", host_ctr[33] / tot);
+        if (host_ctr[35])
+            std::fprintf(stderr, "rtow-profile: Box leaf scans in node steps %.3f per ray, %.1f lanes per wave scan\n",
+                         (double)host_ctr[34] / std::max(1ull, host_ctr[0]), (double)host_ctr[34] / host_ctr[35]);
     }
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
     if (host_ctr[13])
