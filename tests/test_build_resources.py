@@ -26,7 +26,7 @@ LIB = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "librtow_hip.so")
 # by MODE (see DESIGN.md "Kernels"); the simple-scene kernels get none.
 # (xhit's call frames live in a global buffer, DevParams::xframes, not in
 # scratch: a private array sized every wave's scratch for it.)
-SCRATCH_BOUND = {0: 0, 2: 64, 4: 64, 3: 160, 5: 48, 6: 16}
+SCRATCH_BOUND = {0: 0, 2: 0, 4: 16, 3: 96, 5: 0, 6: 0}
 
 
 @pytest.fixture(scope="module")
