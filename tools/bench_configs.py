@@ -35,7 +35,10 @@ def pmc_roofline(scene, W, H, segments, kernel_ms, src_hash):
     import glob
 
     best = None
-    for f in glob.glob(os.path.join(HERE, "..", "profiles", "*", "pmc_summary.json")):
+    # (gpurun_out/prof_*: the summaries tools/round_check.sh wrote earlier in
+    # the same GPU call, before they are copied into profiles/)
+    for f in (glob.glob(os.path.join(HERE, "..", "profiles", "*", "pmc_summary.json")) +
+              glob.glob(os.path.join(HERE, "..", "gpurun_out", "prof_*", "pmc_summary.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):

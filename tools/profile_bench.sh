@@ -1,12 +1,13 @@
 #!/bin/bash
 # Profiles of the bench configuration (run on the GPU box from the repo root):
-#   1. bench.py itself (the line the driver parses, CPU baseline included),
-#   2. rocprofv3 --kernel-trace --stats of bench.py (per-kernel durations),
-#   3. PMC passes, one counter group per run with --kernel-trace beside it
+#   1. rocprofv3 --kernel-trace --stats of bench.py (per-kernel durations),
+#   2. PMC passes, one counter group per run with --kernel-trace beside it
 #      only (never a trace domain), each over ONE bench step (one launch),
 # then tools/pmc_summarize.py writes pmc_summary.json: the trace kernel's
 # counters per launch, tagged with the build's source hash, the config and
-# the rays of that launch -- what bench.py's VALU roofline reads.
+# the rays of that launch -- what bench.py's VALU roofline reads; and last
+#   3. bench.py itself (the line the driver parses, CPU baseline included),
+#      its roofline from that summary.
 #   bash tools/profile_bench.sh TAG [extra bench.py args, e.g. --workload cornell]
 # Output: gpurun_out/prof_TAG/ (copy bench.json, kernel_stats.csv and
 # pmc_summary.json into profiles/TAG/).
@@ -18,7 +19,6 @@ R=$(pwd)
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python3 bench.py $EXTRA > $OUT/bench.json 2> $OUT/bench.err || exit $?
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
     python3 $R/bench.py --steps 2 --warmup 1 --no-cpu $EXTRA > $OUT/trace.log 2>&1 || exit $?
@@ -32,4 +32,6 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
       python3 $R/bench.py --steps 1 --warmup 0 --no-cpu $EXTRA > $OUT/p$i.log 2>&1 || exit $?
 done
 cd $R
-python3 tools/pmc_summarize.py $OUT
+python3 tools/pmc_summarize.py $OUT || exit $?
+# the bench line last, its roofline from the counters just summarized
+timeout -k 10 300 python3 bench.py $EXTRA --pmc-json $OUT/pmc_summary.json > $OUT/bench.json 2> $OUT/bench.err || exit $?
