@@ -92,6 +92,8 @@ def parse(argv=None):
                     help="pixels of the CPU baseline's sample (default: ~10-20 s of the reference's work)")
     ap.add_argument("--cpu-spp", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-prime", action="store_true",
+                    help="skip the 1-spp render that loads the code objects (profiling: every trace-kernel launch is a step)")
     ap.add_argument("--cpu-kind", choices=["auto", "port"], default="auto",
                     help="auto: the reference's own code when oracle/_ref was built, else the oracle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every host CPU this process may use")
@@ -336,8 +338,9 @@ class HipRank:
         self.stream = torch.cuda.current_stream().cuda_stream
         self.p = rtow.params(W, H, args.spp, seed=args.seed, rank=rank, world=world)
         # load the code objects once (not a step: the warmup steps stay the contract's)
-        self.ctx.render_tiles_device(self.cam, rtow.params(W, H, 1, seed=args.seed, rank=rank, world=world),
-                                     self.slab.data_ptr(), None, self.stream)
+        if not args.no_prime:
+            self.ctx.render_tiles_device(self.cam, rtow.params(W, H, 1, seed=args.seed, rank=rank, world=world),
+                                         self.slab.data_ptr(), None, self.stream)
         torch.cuda.synchronize()
 
     def init_kwargs(self):

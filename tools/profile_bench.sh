@@ -1,6 +1,7 @@
 #!/bin/bash
 # Profiles of the bench configuration (run on the GPU box from the repo root):
-#   1. rocprofv3 --kernel-trace --stats of bench.py (per-kernel durations),
+#   1. rocprofv3 --kernel-trace --stats of bench.py (per-kernel durations;
+#      3 steps, no prime launch: every trace-kernel call is a bench step),
 #   2. PMC passes, one counter group per run with --kernel-trace beside it
 #      only (never a trace domain), each over ONE bench step (one launch),
 # then tools/pmc_summarize.py writes pmc_summary.json: the trace kernel's
@@ -21,7 +22,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu $EXTRA > $OUT/trace.log 2>&1 || exit $?
+    python3 $R/bench.py --steps 3 --warmup 0 --no-prime --no-cpu $EXTRA > $OUT/trace.log 2>&1 || exit $?
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE" \
