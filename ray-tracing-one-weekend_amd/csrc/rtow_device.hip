@@ -900,14 +900,14 @@ struct Best {
 // hit(t1 + 0.0001, FLT_MAX) then rejects the near root again and takes the
 // far one -- the same roots Sphere::hit (sphere.h:20-69) computes each call.
 template <bool UNIT_TIME>
-__device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, float a, float& t1, float& t2) {
+__device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, float a, float ra, float& t1, float& t2) {
     const F3 oc = sub(r.o, sph_center<UNIT_TIME>(s, r.time));
     const float b = dot(r.d, oc);
     const float c = dot(oc, oc) - s.r * s.r;
     const float disc = b * b - a * c;
     if (!(disc > 0)) return false;
     const float sq = sqrtf(disc);
-    const float tn = (-b - sq) / a, tf = (-b + sq) / a;
+    const float tn = div_by(-b - sq, a, ra), tf = div_by(-b + sq, a, ra);  // the IEEE quotients (sph_root's)
     const float lo = -FLT_MAX;
     float first;
     if (tn < FLT_MAX && tn > lo) first = tn;
@@ -933,15 +933,16 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                                          uint32_t prev, Prof* prof = nullptr);
 
 template <int STACK, bool ANYB>
-__device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, const Ray& wray,
-                                           float tmin, float& bt, uint32_t* stk, int sp, Rng& rng, uint32_t& overflow) {
+__device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, float ra,
+                                           const Ray& wray, float tmin, float& bt, uint32_t* stk, int sp, Rng& rng,
+                                           uint32_t& overflow) {
     const DMedium M = S.med[idx];
     (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
     float t1 = 0, t2 = 0;
     bool two = false;
     if (M.bkind == MB_SPHERE) {
         const Sph s = load_sph(S.sph + (M.boundary & INDEX_MASK));
-        two = S.unit_time ? sphere_boundary<true>(s, r, a, t1, t2) : sphere_boundary<false>(s, r, a, t1, t2);
+        two = S.unit_time ? sphere_boundary<true>(s, r, a, ra, t1, t2) : sphere_boundary<false>(s, r, a, ra, t1, t2);
     } else if (M.bkind == MB_BOX6) {
         // the same two queries over a Box's sides (box6_nearest)
         const Ray rb = chain_ray(S, M.bchain, wray);
@@ -999,7 +1000,7 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
             if (ta < 0) ta = 0;
             const float dl = len(r.d);
             const float inside = (tb - ta) * dl;
-            const float dist = (float)(-(1 / M.density) * log(rng.next()));
+            const float dist = (float)(-M.inv_density * log(rng.next()));
             if (dist < inside) {
                 bt = ta + dist / dl;
                 return true;
@@ -1166,7 +1167,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
                     ref_skips_hit(S, best.prim & LEAF_MASK, wray, bt, tmin))
                     overflow |= 2u;  // see traverse_top's TOP_MEDIUM
                 tmed = __builtin_nanf("");
-                if (medium_hit<STACK, ANYB>(S, idx, r, a, wray, tmin, tm, stk, sp, rng, overflow) &&
+                if (medium_hit<STACK, ANYB>(S, idx, r, a, ra, wray, tmin, tm, stk, sp, rng, overflow) &&
                     take_hit(S, tm, bt, best.prim, cur))
                     found = true;
             }
@@ -1262,11 +1263,11 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             if constexpr (PARK) {
                 uint32_t* const cw = stk + (size_t)STACK * BLOCK;
                 Rng m{(uint64_t)cw[15 * BLOCK] << 32 | cw[14 * BLOCK], cw[16 * BLOCK]};
-                if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, m, overflow))
+                if (medium_hit<STACK, false>(S, T.a, r, a, ra, wray, tmin, bt, stk, 0, m, overflow))
                     bp = mkref(DK_MEDIUM, T.a);
                 cw[16 * BLOCK] = m.ctr;
             } else {
-                if (medium_hit<STACK, false>(S, T.a, r, a, wray, tmin, bt, stk, 0, rng, overflow))
+                if (medium_hit<STACK, false>(S, T.a, r, a, ra, wray, tmin, bt, stk, 0, rng, overflow))
                     bp = mkref(DK_MEDIUM, T.a);
             }
         } else if (kind == TOP_SPHERES) {
@@ -3501,7 +3502,7 @@ struct Converter {
             ref = mkref(DK_MEDIUM, slot);
             memo[hi] = ref;
             uint32_t b = conv(h.a, underBvh);
-            L.med[slot] = DMedium{b, h.b, h.f[0], 0};
+            L.med[slot] = DMedium{b, h.b, 1.0f / h.f[0], 0};
             break;
         }
         default:

@@ -141,7 +141,7 @@ struct alignas(16) DBox6 {  // 32 B
 enum : uint32_t { MB_ANY = 0, MB_SPHERE = 1, MB_RECTS = 2, MB_BOX6 = 3 };  // MB_BOX6: bfirst = box6 index
 struct alignas(16) DMedium {  // 32 B, constantMedium.h:21-23
     uint32_t boundary, phase_mat;
-    float density;
+    float inv_density;  // 1 / density, the float quotient constantMedium.h:47 forms (host IEEE division)
     uint32_t chain;
     uint32_t bkind, bfirst, bcount, bchain;
 };
