@@ -167,10 +167,23 @@ __device__ __forceinline__ Ray root_ray(const DevScene& S, const Ray& w) {
 
 // the ray in the frame of chain `id` (DevScene::chains), outermost first
 __device__ __forceinline__ Ray chain_ray(const DevScene& S, uint32_t id, const Ray& w) {
-    const DChain& C = S.chains[id];
+    const DChainX& C = S.chains[id];
     const int n = (int)C.n;
     Ray r = w;
-    for (int k = 0; k < n; k++) r = apply_inst(S, C.ref[k], r);
+    for (int k = 0; k < n; k++) {
+        const float4 e = C.t[k];
+        const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
+        if (kind == DK_TRANSLATE) {
+            r.o = sub(r.o, f3(e.y, e.z, e.w));
+        } else if (kind == DK_ROTY) {  // apply_inst's operations
+            const float sn = e.y, c = e.z;
+            const F3 o = r.o, d = r.d;
+            r.o.x = c * o.x - sn * o.z;
+            r.o.z = sn * o.x + c * o.z;
+            r.d.x = c * d.x - sn * d.z;
+            r.d.z = sn * d.x + c * d.z;
+        }
+    }
     return r;
 }
 
@@ -179,8 +192,25 @@ __device__ __forceinline__ void inst_out(const DevScene& S, uint32_t ref, F3& p,
 
 // the way out of the instances, innermost first
 __device__ __forceinline__ void chain_out(const DevScene& S, uint32_t id, F3& p, F3& nrm) {
-    const DChain& C = S.chains[id];
-    for (int k = (int)C.n - 1; k >= 0; k--) inst_out(S, C.ref[k], p, nrm);
+    const DChainX& C = S.chains[id];
+    for (int k = (int)C.n - 1; k >= 0; k--) {  // inst_out's operations
+        const float4 e = C.t[k];
+        const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
+        if (kind == DK_FLIP) {
+            nrm = neg(nrm);
+        } else if (kind == DK_TRANSLATE) {
+            p = add(p, f3(e.y, e.z, e.w));
+        } else {
+            const float sn = e.y, c = e.z;
+            F3 q = p, m = nrm;
+            q.x = c * p.x + sn * p.z;
+            q.z = -sn * p.x + c * p.z;
+            m.x = c * nrm.x + sn * nrm.z;
+            m.z = -sn * nrm.x + c * nrm.z;
+            p = q;
+            nrm = m;
+        }
+    }
 }
 
 __device__ __forceinline__ void root_out(const DevScene& S, F3& p, F3& nrm) {
@@ -4516,7 +4546,21 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_refs = pushBlob(blob, L.refs), o_med = pushBlob(blob, L.med), o_mat = pushBlob(blob, L.mat);
     size_t o_tex = pushBlob(blob, L.tex), o_rv = pushBlob(blob, L.ranvec), o_perm = pushBlob(blob, L.perm);
     size_t o_img = pushBlob(blob, L.img), o_texels = pushBlob(blob, L.texels);
-    size_t o_ch = pushBlob(blob, L.chains);
+    std::vector<DChainX> chainx(L.chains.size());
+    for (size_t c = 0; c < L.chains.size(); c++) {
+        const DChain& C = L.chains[c];
+        DChainX& X = chainx[c];
+        X.n = C.n;
+        for (uint32_t k = 0; k < C.n && k < (uint32_t)MAXCHAIN; k++) {
+            const DInst& I = L.inst[C.ref[k] & INDEX_MASK];
+            uint32_t rb = C.ref[k];
+            float rf;
+            std::memcpy(&rf, &rb, 4);
+            X.t[k] = make_float4(rf, I.p[0], I.p[1], I.p[2]);
+        }
+    }
+    if (chainx.empty()) chainx.push_back(DChainX{});
+    size_t o_ch = pushBlob(blob, chainx);
     size_t o_ks = pushBlob(blob, L.sph_key), o_kr = pushBlob(blob, L.rect_key), o_km = pushBlob(blob, L.med_key);
     std::vector<DTop> top = L.top;
     if (top.empty()) top.push_back(DTop{});
@@ -4559,7 +4603,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.perm = (const uint32_t*)(b + o_perm);
     d.img = (const DImage*)(b + o_img);
     d.texels = (const uint8_t*)(b + o_texels);
-    d.chains = (const DChain*)(b + o_ch);
+    d.chains = (const DChainX*)(b + o_ch);
     d.sph_key = (const unsigned long long*)(b + o_ks);
     d.rect_key = (const unsigned long long*)(b + o_kr);
     d.med_key = (const unsigned long long*)(b + o_km);

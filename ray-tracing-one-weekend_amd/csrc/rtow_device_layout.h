@@ -116,6 +116,13 @@ struct alignas(16) DChain {  // 32 B: instance refs, outermost first
     uint32_t n;
     uint32_t ref[MAXCHAIN];
 };
+// The device's copy of a chain: the instances' parameters inline (no second
+// dependent load per chain walk): per instance (ref bits, p0, p1, p2) --
+// Translate offset, or RotateY sine and cosine (DInst::p)
+struct alignas(16) DChainX {  // 128 B
+    float4 t[MAXCHAIN];
+    uint32_t n, pad[3];
+};
 
 struct alignas(16) DList {  // 16 B: children at refs[first .. first+count)
     uint32_t first, count;
@@ -220,7 +227,7 @@ struct DevScene {
     const DList* list;
     const uint32_t* refs;
     const DMedium* med;
-    const DChain* chains;
+    const DChainX* chains;
     const DTop* top;         // general scenes: the top-level list, n_top items (0: none)
     const DProg* prog;       // programs of the BvhNode subtrees that hold media (DK_PROG)
     const DBox6* box6;       // Boxes among the rectangle lists (DList::box6, TOP_BOX6, MB_BOX6)
