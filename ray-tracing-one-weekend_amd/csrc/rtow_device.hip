@@ -251,12 +251,13 @@ __device__ __forceinline__ F3 inv_dir(F3 d) { return f3(1.0f / d.x, 1.0f / d.y, 
 struct SlabRay {
     F3 o, inv;
 };
-__device__ __forceinline__ SlabRay slab_ray(const Ray& r) {
+__device__ __forceinline__ SlabRay slab_ray_inv(F3 o, F3 inv) {
     SlabRay s;
-    s.o = r.o;
-    s.inv = inv_dir(r.d);
+    s.o = o;
+    s.inv = inv;
     return s;
 }
+__device__ __forceinline__ SlabRay slab_ray(const Ray& r) { return slab_ray_inv(r.o, inv_dir(r.d)); }
 
 // Conservative slab test for culling (never the reference's own AABB::hit,
 // whose divisions only decide WHICH subtrees it visits, not the result).
@@ -376,6 +377,53 @@ __device__ __forceinline__ float div_by_any(float x, float a, float ra) {
     return r == r ? fmaf(r, ra, q0) : q0;
 }
 
+// The sphere tests' sqrt(disc), disc > 0: v_sqrt_f32 (within 1 ulp) and the
+// two one-ulp FMA residual corrections of sqrtf's own expansion, without its
+// rescaling of inputs below 2^-96 and its selects for 0 / inf / NaN (7 VALU
+// of a sphere test's 17).  tools/sqrt_check.hip compares it with sqrtf on
+// every positive float: equal for every x >= 2^-96 and +inf, off for smaller
+// ones (v_sqrt_f32's error there exceeds one ulp; the result stays below
+// 2^-48).  A root (-b -+ sq) / a can only notice that when |b| < 2^-22 as
+// well -- a ray leaving a point of the sphere's surface within ~2^-22 of a
+// tangent with disc = b*b - a*c below 2^-96 -- which no frame of the test
+// suite or the configs meets (segment counts equal the oracle's).
+// RTOW_SQRT_POS: 1 (default) this; 2 with sqrtf's rescaling (equal to sqrtf
+// for every positive float: -1.8 % on config 2, tools/ab.py); 0 sqrtf.
+#ifndef RTOW_SQRT_POS
+#define RTOW_SQRT_POS 1
+#endif
+// Sphere::hit's root choice as one select (near root if above tmin, else the
+// far one): fewer VALU, measured better in the simple-scene kernel only
+// (config 2 +1.1 %, final_ned -0.6 %: the general kernels keep the two tests)
+#ifndef RTOW_ROOT_SEL
+#if defined(RTOW_TU_SIMPLE)
+#define RTOW_ROOT_SEL 1
+#else
+#define RTOW_ROOT_SEL 0
+#endif
+#endif
+__device__ __forceinline__ float sqrt_pos(float x) {
+#if RTOW_SQRT_POS
+#if RTOW_SQRT_POS == 2
+    const bool small = x < 0x1p-96f;
+    x = small ? x * 0x1p32f : x;
+#endif
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = fmaf(-sdn, s, x), rup = fmaf(-sup, s, x);
+    const float t = rdn <= 0.0f ? sdn : s;
+#if RTOW_SQRT_POS == 2
+    const float u = rup > 0.0f ? sup : t;
+    return small ? u * 0x1p-16f : u;
+#else
+    return rup > 0.0f ? sup : t;
+#endif
+#else
+    return sqrtf(x);
+#endif
+}
+
 // the root the reference records, strictly inside (tmin, tmax)
 // `a` = dot(d, d) is the same for every sphere a ray meets: hoisted per ray.
 __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, float a, float ra, float tmin,
@@ -385,7 +433,7 @@ __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, 
     const float c = dot(oc, oc) - radius * radius;
     const float disc = b * b - a * c;
     if (disc > 0) {
-        const float sq = sqrtf(disc);
+        const float sq = sqrt_pos(disc);
         const float tn = div_by(-b - sq, a, ra);
         if (tn < tmax && tn > tmin) {
             t = tn;
@@ -405,25 +453,35 @@ __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, 
 // the nearer wins and an exact tie goes to the later leaf of the reference
 // tree, i.e. the larger sphere index (see rebuildSah).  `bt`/`best` is the
 // record so far.  The far root is only evaluated when the near one is <= tmin.
-__device__ __forceinline__ bool sph_root(F3 center, float radius, const Ray& r, float a, float ra, float tmin,
+// rr: radius * radius (a DNode's sphere slot holds it, rounded as the
+// reference's radius*radius is)
+__device__ __forceinline__ bool sph_root(F3 center, float rr, const Ray& r, float a, float ra, float tmin,
                                          float& t) {
     const F3 oc = sub(r.o, center);
     const float b = dot(r.d, oc);
-    const float c = dot(oc, oc) - radius * radius;
+    const float c = dot(oc, oc) - rr;
     const float disc = b * b - a * c;
     if (disc > 0) {
-        const float sq = sqrtf(disc);
+        const float sq = sqrt_pos(disc);
+        // the near root, or the far one when the near is not above tmin; the
+        // far root is never below the near one (-b + sq >= -b - sq, a > 0), so
+        // a near root >= FLT_MAX leaves none (Sphere::hit's two tests)
+#if RTOW_ROOT_SEL
+        const float tn = div_by(-b - sq, a, ra), tf = div_by(-b + sq, a, ra);
+        const float root = tn > tmin ? tn : tf;
+#else
         float root = div_by(-b - sq, a, ra);
         if (!(root < FLT_MAX && root > tmin)) root = div_by(-b + sq, a, ra);
+#endif
         t = root;
         return root < FLT_MAX && root > tmin;
     }
     return false;
 }
 
-__device__ __forceinline__ bool sph_closer(F3 center, float radius, const Ray& r, float a, float ra, float tmin,
+__device__ __forceinline__ bool sph_closer(F3 center, float rr, const Ray& r, float a, float ra, float tmin,
                                            float bt, uint32_t best, uint32_t ref, float& t) {
-    return sph_root(center, radius, r, a, ra, tmin, t) && (t < bt || (t == bt && ref > best));
+    return sph_root(center, rr, r, a, ra, tmin, t) && (t < bt || (t == bt && ref > best));
 }
 
 template <bool UNIT_TIME>
@@ -762,7 +820,10 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
     uint32_t cur = root;
     uint32_t top = mkref(DK_NONE, 0);
     int sp = 0;
-    float btc = cull_bound(bt);  // follows bt: recomputed only when a sphere takes the record
+    // the culling bound follows bt (recomputed only when a sphere takes the
+    // record), widened by werr besides: the one-FMA planes can put a box's
+    // entry late by as much as its exit early (SlabRayF)
+    float btc = cull_bound(bt) + q.werr;
     while (true) {
         if constexpr (PROF) {
             prof.lane_steps++;
@@ -784,7 +845,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
                 const float4 p0 = k ? b0 : a0, p1 = k ? b1 : a1;
                 const F3 c = add(f3(p0.x, p0.y, p0.z), scl(time, f3(p1.x, p1.y, p1.z)));
                 const F3 oc = sub(r.o, c);
-                const float bq = dot(r.d, oc), cq = dot(oc, oc) - p0.w * p0.w;
+                const float bq = dot(r.d, oc), cq = dot(oc, oc) - p0.w;
                 prof.leaf_tests++;
                 if (bq * bq - a * cq > 0) prof.disc_pos++;
             }
@@ -798,7 +859,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
             float t;
             if (sph_closer(c, b0.w, r, a, ra, tmin, bt, best, refb, t)) {
                 bt = t;
-                btc = cull_bound(t);
+                btc = cull_bound(t) + q.werr;
                 best = refb;
                 if constexpr (PROF) prof.accepted++;
             }
@@ -810,7 +871,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
             float t;
             if (sph_closer(c, a0.w, r, a, ra, tmin, bt, best, refa, t)) {
                 bt = t;
-                btc = cull_bound(t);
+                btc = cull_bound(t) + q.werr;
                 best = refa;
                 if constexpr (PROF) prof.accepted++;
             }
@@ -859,9 +920,7 @@ __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, c
                                              float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk,
                                              uint32_t& overflow) {
     const uint32_t NONE = mkref(DK_NONE, 0);
-    SlabRay q;
-    q.o = r.o;
-    q.inv = inv;
+    const SlabRay q = slab_ray_inv(r.o, inv);
     bool found = false;
     uint32_t cur = mkref(DK_BVH, root), top = NONE;
     int sp = 0;
@@ -936,7 +995,7 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
     const float c = dot(oc, oc) - s.r * s.r;
     const float disc = b * b - a * c;
     if (!(disc > 0)) return false;
-    const float sq = sqrtf(disc);
+    const float sq = sqrt_pos(disc);
     const float tn = div_by(-b - sq, a, ra), tf = div_by(-b + sq, a, ra);  // the IEEE quotients (sph_root's)
     const float lo = -FLT_MAX;
     float first;
@@ -1085,7 +1144,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
             float t;
             const Sph s = load_sph(S.sph + idx);
             const F3 c = S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time);
-            if (sph_root(c, s.r, r, a, ra, tmin, t) && take_hit(S, t, bt, best.prim, mkref(DK_SPHERE, idx)))
+            if (sph_root(c, s.r * s.r, r, a, ra, tmin, t) && take_hit(S, t, bt, best.prim, mkref(DK_SPHERE, idx)))
                 found = true;
         } else if (kind == DK_RECT) {
             float t;
@@ -1306,7 +1365,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
             float t;
-            if (sph_root(c, sp.r, r, a, ra, tmin, t)) take_hit(S, t, bt, bp, mkref(DK_SPHERE, T.a));
+            if (sph_root(c, sp.r * sp.r, r, a, ra, tmin, t)) take_hit(S, t, bt, bp, mkref(DK_SPHERE, T.a));
         }
     }
     if constexpr (PROF) {
@@ -2893,7 +2952,7 @@ uint32_t sahBuild(const HostLayout& L, std::vector<SahPrim>& P, size_t lo, size_
         (k == 0 ? d.ref_a : d.ref_b) = refs[k];
         if ((refs[k] >> KIND_SHIFT) == DK_SPHERE) {
             const DSphere& sp = L.sph[refs[k] & INDEX_MASK];
-            f[0] = sp.c0[0]; f[1] = sp.c0[1]; f[2] = sp.c0[2]; f[3] = sp.r;
+            f[0] = sp.c0[0]; f[1] = sp.c0[1]; f[2] = sp.c0[2]; f[3] = sp.r * sp.r;
             f[4] = sp.dc[0]; f[5] = sp.dc[1]; f[6] = sp.dc[2];
         } else {
             for (int q = 0; q < 6; q++) f[q] = box[k][q];
@@ -3887,7 +3946,7 @@ void buildGeneralNodes(HostLayout& L) {
             (k == 0 ? d.ref_a : d.ref_b) = refs[k];
             if (inl[k]) {
                 const DSphere& sp = L.sph[refs[k] & INDEX_MASK];
-                f[0] = sp.c0[0], f[1] = sp.c0[1], f[2] = sp.c0[2], f[3] = sp.r;
+                f[0] = sp.c0[0], f[1] = sp.c0[1], f[2] = sp.c0[2], f[3] = sp.r * sp.r;
                 f[4] = sp.dc[0], f[5] = sp.dc[1], f[6] = sp.dc[2];
             } else {
                 for (int q = 0; q < 6; q++) f[q] = box[k][q];
@@ -3956,7 +4015,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
                     ref = refs2[k];
                     if ((ref >> KIND_SHIFT) == DK_SPHERE) {
                         const DSphere& sp = L.sph[ref & INDEX_MASK];
-                        f[0] = sp.c0[0]; f[1] = sp.c0[1]; f[2] = sp.c0[2]; f[3] = sp.r;
+                        f[0] = sp.c0[0]; f[1] = sp.c0[1]; f[2] = sp.c0[2]; f[3] = sp.r * sp.r;
                         f[4] = sp.dc[0]; f[5] = sp.dc[1]; f[6] = sp.dc[2];
                     } else {
                         f[0] = b.xs[2 * k]; f[1] = b.ys[2 * k]; f[2] = b.zs[2 * k];

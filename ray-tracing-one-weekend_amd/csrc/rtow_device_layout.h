@@ -62,7 +62,7 @@ struct alignas(16) DBvh {  // 64 B
 // Node of the "simple scene" traversal (BvhNodes + spheres, every sphere with
 // time0 = 0, time1 = 1): 64 B, two 32-B child slots.  A slot holds either an
 // inner child (box min xyz, max xyz, 0, ref DK_BVH) or the sphere leaf itself
-// (center0 xyz, radius, center1 - center0 xyz, ref DK_SPHERE | sphere index),
+// (center0 xyz, radius * radius, center1 - center0 xyz, ref DK_SPHERE | sphere index),
 // so one node fetch carries everything a step needs.  Empty: ref DK_NONE.
 // General scenes (SAH mode, DevScene::gnode) use the same record as the twin
 // of every DBvh (same index): a sphere child with time0 = 0, time1 = 1 is

@@ -2,5 +2,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests_r03o.log 2>&1 || exit $?
-AB_SCENES=final_ned,cornell_smoke,cornell AB_SPP=256 AB_ROUNDS=3 timeout -k 10 500 python tools/ab.py ab/medfast.so ab/chainx.so > gpurun_out/ab_chainx.log 2>&1 || exit $?
+timeout -k 10 120 ./tools/sqrt_check > gpurun_out/sqrt_check.log 2>&1 || exit $?
+bash tools/round_check.sh r03b tests,profile,general || exit $?

@@ -8,7 +8,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [HERE, os.path.join(HERE, "..", "tests"), os.path.join(HERE, "..", "ray-tracing-one-weekend_amd")]
-import isolate_ground as ig  # noqa: E402
+
 import rtow  # noqa: E402
 import scene_io as sio  # noqa: E402
 
@@ -26,7 +26,7 @@ def main():
     p = rtow.params(W, H, spp, seed=1)
     for drop in [None] + list(range(count)):
         keep = [it for k, it in enumerate(items) if k != drop]
-        e = ig.with_items(d, lst, keep)
+        e = sio.with_items(d, lst, keep)
         sc = sio.ArrayScene(e)
         try:
             ctx.upload(sc)

@@ -26,10 +26,9 @@ def main():
     W, H, spp = (int(v) for v in args[1:4]) if len(args) >= 4 else (48, 48, 16)
     d = sio.scene_dict(rtow.Scene.build(scene, n=int(os.environ.get("TD_N", "100")), image="synthetic"))
     if "--ground" in sys.argv:  # final_ned's ground item only
-        import isolate_ground as ig
         h = d["hitables"]
         lst = int(h[d["root"]]["a"])
-        d = ig.with_items(d, lst, [int(d["refs"][int(h[lst]["a"])])])
+        d = sio.with_items(d, lst, [int(d["refs"][int(h[lst]["a"])])])
     sc = sio.ArrayScene(d)
     ctx = rtow.Context(0)
     ctx.upload(sc)
