@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -864,7 +865,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            hb = slab_f(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
+            hb = slab_f(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb);  // (a simple scene's slot: sphere or DK_BVH)
         }
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
@@ -876,7 +877,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
                 if constexpr (PROF) prof.accepted++;
             }
         } else {
-            ha = slab_f(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
+            ha = slab_f(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta);
         }
         // one back-edge, one exit: push / descend / pop are predicated updates
         const uint32_t NONE = mkref(DK_NONE, 0);
@@ -884,13 +885,12 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
         const bool both = ha && hb;
         uint32_t nxt = both ? (afirst ? refa : refb) : (ha ? refa : (hb ? refb : NONE));
         if (both) {  // push the farther child; the old top goes to LDS
+            // (no bound check: the host's stack_need, the deepest chain of
+            // nodes with two inner children, is at most STACK, and the
+            // register top holds one of those entries: checkSimpleNodes)
             if (top != NONE) {
-                if (sp < STACK) {
-                    stk[sp * BS] = top;
-                    sp++;
-                } else {
-                    overflow = 1;  // reported as an error by the host
-                }
+                stk[sp * BS] = top;
+                sp++;
             }
             top = afirst ? refb : refa;
         }
@@ -3374,6 +3374,31 @@ void shiftBoxes(HostLayout& L) {
     for (int a = 0; a < 3; a++) L.tshift[a] = t[a];
 }
 
+// What trace_simple relies on without checking it per step: every slot of
+// the DNodes reachable from the root is a sphere or an inner node (no
+// DK_NONE), and no chain of nodes with two inner children is longer than the
+// stack_need the kernel's STACK is chosen by (launchStack: need <= STACK).
+bool checkSimpleNodes(const HostLayout& L) {
+    if ((L.bvh_root >> KIND_SHIFT) != DK_BVH) return (L.bvh_root >> KIND_SHIFT) == DK_SPHERE;
+    std::vector<uint32_t> memo(L.node.size(), ~0u);
+    std::function<uint32_t(uint32_t, int)> need = [&](uint32_t i, int depth) -> uint32_t {
+        if (i >= L.node.size() || depth > 4096) return ~0u;
+        if (memo[i] != ~0u) return memo[i];
+        const DNode& d = L.node[i];
+        uint32_t n[2] = {0, 0};
+        bool inner[2];
+        for (int k = 0; k < 2; k++) {
+            const uint32_t ref = k == 0 ? d.ref_a : d.ref_b, kind = ref >> KIND_SHIFT;
+            inner[k] = kind == DK_BVH;
+            if (kind != DK_SPHERE && kind != DK_BVH) return ~0u;
+            if (inner[k] && (n[k] = need(ref & INDEX_MASK, depth + 1)) == ~0u) return ~0u;
+        }
+        return memo[i] = (inner[0] && inner[1]) ? 1 + std::max(n[0], n[1]) : std::max(n[0], n[1]);
+    };
+    const uint32_t n = need(L.bvh_root & INDEX_MASK, 0);
+    return n != ~0u && n <= L.stack_need;
+}
+
 // true when everything below `ref` is BvhNodes and spheres
 bool onlyBvhSpheres(const HostLayout& L, uint32_t ref, int depth = 0) {
     const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
@@ -4026,6 +4051,7 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
             }
             if (tree == RTOW_TREE_SAH && (L.bvh_root >> KIND_SHIFT) == DK_BVH) rebuildSah(L);
             shiftBoxes(L);
+            if (!checkSimpleNodes(L)) return set_error(RTOW_E_INVALID, "internal: simple-scene tree check failed");
         }
     }
     for (uint32_t i = 0; i < s.n_materials; i++) {
