@@ -820,11 +820,22 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
     }
     uint32_t cur = root;
     uint32_t top = mkref(DK_NONE, 0);
-    int sp = 0;
+    // entry 0 of the LDS stack holds NONE, a sentinel no push overwrites
+    // (entries live at 1 .. sp - 1): a pop reads entry sp - 1 and keeps sp >= 1,
+    // no branch -- from the empty stack it reads the sentinel.  The capacity
+    // of STACK - 1 entries still covers the host's stack_need - 1 (the register
+    // top holds one more).
+    stk[0] = mkref(DK_NONE, 0);
+    int sp = 1;
     // the culling bound follows bt (recomputed only when a sphere takes the
     // record), widened by werr besides: the one-FMA planes can put a box's
     // entry late by as much as its exit early (SlabRayF)
     float btc = cull_bound(bt) + q.werr;
+    // the record as one 64-bit key, (t bits, ~leaf): t > tmin > 0 and bt are
+    // positive, so their bits order as the floats do, and ~ reverses the leaf
+    // order -- key < record  <=>  t < bt || (t == bt && leaf > best), the
+    // reference's tie rule (sph_closer), in one 64-bit compare
+    unsigned long long rkey = (unsigned long long)__float_as_uint(bt) << 32 | (uint32_t)~best;
     while (true) {
         if constexpr (PROF) {
             prof.lane_steps++;
@@ -858,11 +869,13 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
             // Sphere::hit / MovingSphere::hit with center = c0 + time * (c1 - c0)
             const F3 c = add(f3(b0.x, b0.y, b0.z), scl(time, f3(b1.x, b1.y, b1.z)));
             float t;
-            if (sph_closer(c, b0.w, r, a, ra, tmin, bt, best, refb, t)) {
-                bt = t;
-                btc = cull_bound(t) + q.werr;
-                best = refb;
-                if constexpr (PROF) prof.accepted++;
+            if (sph_root(c, b0.w, r, a, ra, tmin, t)) {
+                const unsigned long long k = (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)~refb;
+                if (k < rkey) {
+                    rkey = k;
+                    btc = cull_bound(t) + q.werr;
+                    if constexpr (PROF) prof.accepted++;
+                }
             }
         } else {
             hb = slab_f(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb);  // (a simple scene's slot: sphere or DK_BVH)
@@ -870,11 +883,13 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
             float t;
-            if (sph_closer(c, a0.w, r, a, ra, tmin, bt, best, refa, t)) {
-                bt = t;
-                btc = cull_bound(t) + q.werr;
-                best = refa;
-                if constexpr (PROF) prof.accepted++;
+            if (sph_root(c, a0.w, r, a, ra, tmin, t)) {
+                const unsigned long long k = (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)~refa;
+                if (k < rkey) {
+                    rkey = k;
+                    btc = cull_bound(t) + q.werr;
+                    if constexpr (PROF) prof.accepted++;
+                }
             }
         } else {
             ha = slab_f(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta);
@@ -896,16 +911,14 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
         }
         if (nxt == NONE) {  // pop
             nxt = top;
-            top = NONE;
-            if (sp > 0) {
-                --sp;
-                top = stk[sp * BS];
-            }
+            top = stk[(sp - 1) * BS];
+            sp = max(sp - 1, 1);
         }
         if (nxt == NONE) break;
         cur = nxt;
     }
-    return best;
+    bt = __uint_as_float((uint32_t)(rkey >> 32));
+    return ~(uint32_t)rkey;
 }
 
 // A BvhNode of unit-time spheres inside a general scene (TOP_SPHERES: a
@@ -939,7 +952,10 @@ __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, c
                 found = true;
             }
         } else {
-            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb) && (refb >> KIND_SHIFT) == DK_BVH;
+            // (a TOP_SPHERES tree's slots are spheres or inner nodes only:
+            // sphereInstance; and the general stack_need counts every one of
+            // its BvhNodes, so the push needs no bound check)
+            hb = slab(b0.x, b0.w, b0.y, b1.x, b0.z, b1.y, q, tmin, btc, tb);
         }
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(r.time, f3(a1.x, a1.y, a1.z)));
@@ -949,19 +965,15 @@ __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, c
                 found = true;
             }
         } else {
-            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta) && (refa >> KIND_SHIFT) == DK_BVH;
+            ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta);
         }
         const bool afirst = ta <= tb;
         const bool both = ha && hb;
         uint32_t nxt = both ? (afirst ? refa : refb) : (ha ? refa : (hb ? refb : NONE));
         if (both) {
             if (top != NONE) {
-                if (sp < STACK) {
-                    stk[sp * BLOCK] = top;
-                    sp++;
-                } else {
-                    overflow = 1;
-                }
+                stk[sp * BLOCK] = top;
+                sp++;
             }
             top = afirst ? refb : refa;
         }
@@ -3396,7 +3408,23 @@ bool checkSimpleNodes(const HostLayout& L) {
         return memo[i] = (inner[0] && inner[1]) ? 1 + std::max(n[0], n[1]) : std::max(n[0], n[1]);
     };
     const uint32_t n = need(L.bvh_root & INDEX_MASK, 0);
-    return n != ~0u && n <= L.stack_need;
+    return n != ~0u && n <= L.stack_need;  // (trace_simple's sentinel: LDS entries <= n - 1 <= STACK - 1)
+}
+
+// every slot of the DNode twins reachable from node i is an inline sphere or
+// an inner node (what trace_dnodes relies on)
+bool sphereNodesOnly(const HostLayout& L, uint32_t i, int depth = 0) {
+    if (i >= L.node.size() || depth > 4096) return false;
+    const DNode& d = L.node[i];
+    for (uint32_t ref : {d.ref_a, d.ref_b}) {
+        const uint32_t k = ref >> KIND_SHIFT;
+        if (k == DK_BVH) {
+            if (!sphereNodesOnly(L, ref & INDEX_MASK, depth + 1)) return false;
+        } else if (k != DK_SPHERE) {
+            return false;
+        }
+    }
+    return true;
 }
 
 // true when everything below `ref` is BvhNodes and spheres
@@ -4167,6 +4195,10 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
     if (!exact && !L.simple) {
         if (tree == RTOW_TREE_SAH) buildTop(L);
         buildGeneralNodes(L);  // DNode twins of the SAH trees, or of the reference's own (RTOW_TREE_REFERENCE)
+        // trace_dnodes (TOP_SPHERES) takes every non-sphere slot for an inner node
+        for (const DTop& t : L.top)
+            if ((t.kind & TOP_KIND_MASK) == TOP_SPHERES && !sphereNodesOnly(L, t.a))
+                return set_error(RTOW_E_INVALID, "internal: TOP_SPHERES tree with a slot that is neither a sphere nor a node");
     }
     if (exact) {
         const int rc = buildExact(s, L);
