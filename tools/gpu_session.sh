@@ -2,9 +2,4 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/gputests_r03u.log 2>&1
-rc=$?
-# test failures (1) still allow the A/B; a hang, a kill or a crash ends the call
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-AB_SCENES=random_ned,final_ned AB_SPP=256 AB_ROUNDS=5 timeout -k 10 600 python -u tools/ab.py ab/v4.so ab/v5.so ab/v6.so > gpurun_out/ab_v6.log 2>&1 || exit $?
-exit $rc
+bash tools/round_check.sh r03c configs,validate || exit $?
