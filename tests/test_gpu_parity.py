@@ -201,6 +201,37 @@ def test_tree_does_not_change_the_frame(scene, n):
     assert np.array_equal(frames[0].view(np.uint32), frames[1].view(np.uint32))
 
 
+@pytest.mark.parametrize("n,need,tree", [(2500, 16, "sah"), (4500, 18, "sah"), (2500, None, "reference")])
+def test_deep_trees_at_the_stack_limit(n, need, tree, gpu_ctx):  # (gpu_ctx: skips without a GPU)
+    """The bench kernel's traversal keeps no per-step stack bound check: the
+    host proves the deepest chain of two-inner nodes fits (checkSimpleNodes)
+    and entry 0 of the LDS stack is a sentinel (capacity STACK - 1, the
+    register top one more).  Random scenes of 2500 spheres (stack_need 16:
+    the STACK=16 kernel at its limit, nodes from global memory) and 4500
+    (18: the STACK=32 kernel), SAH and reference trees, against the oracle:
+    the same segment count, and colours equal but for a last-bit flip."""
+    W, H, spp = 64, 48, 4
+    sc = rtow.Scene.build("random_ned", n=n, image="synthetic")
+    if need is not None:
+        assert sio.scene_check(sc)[0] == need
+    ctx = rtow.Context(0)
+    ctx.set_tree(tree)
+    ctx.upload(sc)
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, spp, seed=5)
+    _, lin, st = ctx.render(cam, p)
+    ctx.close()
+    olin, _, oc = sio.oracle_render(sc.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p)))
+    lin = lin.reshape(-1, 3)
+    d = np.abs(lin.astype(np.float64) - olin).max(axis=1)
+    print(f"DEEP n={n} {tree}: rms {channel_rms(lin, olin)} segments {st.segments} oracle {oc.segments} "
+          f"pixels>1e-3 {int((d > 1e-3).sum())}")
+    assert st.segments == oc.segments  # every path the same length: no closest hit missed
+    # (a last-bit transcendental flip moves one sample of a pixel: ~4e-6 of the pixels at config 2)
+    assert int((d > 1e-3).sum()) <= 1
+
+
 def test_long_flat_list_matches_oracle(gpu_ctx):
     """A HitableList of 400 Boxes (final_ned's ground without its BvhNode) and
     of all random_ned spheres: lists are walked with one continuation entry on
