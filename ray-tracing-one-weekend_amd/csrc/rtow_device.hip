@@ -323,7 +323,9 @@ __device__ __forceinline__ bool slab_f(float x0, float x1, float y0, float y1, f
 // the cancellation of b*b - a*c: its computed t can sit ~2^-10.5 * t before the
 // ray reaches the sphere's box at all (the reference never culls by the best
 // hit, so it still finds that root).  Boxes are culled only beyond t*(1+2^-9).
-__device__ __forceinline__ float cull_bound(float t) { return t + fabsf(t) * 0.001953125f; }
+// t + |t| * 2^-9 with one rounding either way (|t| * 2^-9 is exact): one FMA,
+// the |t| a source modifier (-ffp-contract=off keeps the mul + add otherwise)
+__device__ __forceinline__ float cull_bound(float t) { return fmaf(fabsf(t), 0.001953125f, t); }
 
 // ---- spheres: Sphere::hit sphere.h:20-69 and MovingSphere::hit sphere.h:93-118
 struct Sph {
