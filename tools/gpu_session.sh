@@ -2,4 +2,4 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k deep -v -s --timeout 200 --timeout-method thread > gpurun_out/deep_r03.log 2>&1 || exit $?
+bash tools/round_check.sh r03d || exit $?
