@@ -4390,10 +4390,12 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     // Automatic chunking: the longest items (fewer refills and pixel-sum
     // atomics: on config 2, 64 samples are 4.6 % faster than 16 and 128 another
     // 0.4 %, with 3.6 instead of 16.6 GB of atomic write traffic) that still
-    // leave >= 60 items per lane of the grid (cus x 1024 lanes), so a rank's
-    // share of a multi-GPU frame keeps a short tail (config 2 over 8 ranks:
-    // 16-sample items 0.947 of the ideal, 64-sample 0.877; tools/rank_share.py):
-    // config 2 gets 128 on one GPU, 64 on two, 16 on eight.
+    // leave >= 30 items per lane of the grid (cus x 1024 lanes), so a rank's
+    // share of a multi-GPU frame keeps a short tail.  Config 2's share of 8
+    // ranks (tools/rank_share.py, end of round 3): 64-sample items 151.2 ms,
+    // 32-sample 146.4, 16-sample 149.0 -- round 2's bound of 60 items per lane
+    // picked 16; 30 picks 32.  Config 2 gets 128 on one or two GPUs, 64 on
+    // four, 32 on eight; config 5's shares get 128.
     // RTOW_AUTO_SPC (c->auto_spc) fixes the length instead.
     const uint32_t n_px = rtow_rank_tile_count(p->width, p->height, p->rank, world) * 64u;
     uint32_t spc = p->samples_per_chunk;
@@ -4402,7 +4404,7 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
         const uint64_t lanes = (uint64_t)std::max(1, c->cus) * 1024u;
         spc = 16;
         for (uint32_t cand : {128u, 64u, 32u}) {
-            if ((uint64_t)n_px * ((p->spp + cand - 1) / cand) >= 60 * lanes) {
+            if ((uint64_t)n_px * ((p->spp + cand - 1) / cand) >= 30 * lanes) {
                 spc = cand;
                 break;
             }

@@ -2,4 +2,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-RS_SPC=0 timeout -k 10 300 python -u tools/rank_share.py > gpurun_out/rank_share_r03.txt 2>&1 || exit $?
+RS_SPC=0 timeout -k 10 300 python -u tools/rank_share.py > gpurun_out/rank_share_r03e.txt 2>&1 || exit $?
+bash tools/round_check.sh r03e || exit $?
