@@ -46,7 +46,9 @@ enum {
     RTOW_E_HIP = -3,          /* a HIP runtime call failed */
     RTOW_E_NO_DEVICE = -4,    /* no GPU visible */
     RTOW_E_IO = -5,           /* file read/write failed */
-    RTOW_E_NOMEM = -6
+    RTOW_E_NOMEM = -6,
+    RTOW_E_RCCL = -7          /* an RCCL call failed (rtow_multi_*: the ncclResult and its text
+                                 are kept for rtow_last_error()) */
 };
 
 /* ---- scene graph ---------------------------------------------------------- */
@@ -190,9 +192,9 @@ typedef struct rtow_params {
     uint32_t samples_per_chunk; /* work granularity: a work item is one pixel's chunk of consecutive
                                     samples, summed in float in sample order (main.cpp:946) and added to
                                     the pixel's sum in 192-bit fixed point (order-independent, exact);
-                                    0 = auto (128, 64, 32 or 16: the longest leaving >= 60 items per
+                                    0 = auto (128, 64, 32 or 16: the longest leaving >= 30 items per
                                     lane of the grid, or spp/200 if larger; the last spc..2spc samples
-                                    cut into halving chunks) */
+                                    cut into halving chunks) -- rtow_render_plan shows the choice */
     uint64_t seed;              /* render stream seed (rtow_rng.h) */
     uint32_t rank, world;       /* tile partition; world 0 is treated as 1 */
     uint32_t flags;
@@ -321,6 +323,26 @@ enum {
 };
 int rtow_context_set_tree(rtow_context* ctx, int tree);
 
+/* How a render with `p` cuts its work (diagnostic; host only): the samples per
+ * work item the automatic chunking picks for this device's grid (or
+ * p->samples_per_chunk), the full chunks per pixel, and the halving tail of
+ * the last tail_samples samples in n_tail chunks.  ctx NULL plans for a
+ * 256-CU MI355X without the RTOW_AUTO_SPC override.  The bench's config-2
+ * frame (1920x1080x1024, one rank) gives 128-sample items, n_big 7 and a
+ * 128-sample tail in 8 chunks (64, 32, ..., 1, 1). */
+typedef struct rtow_plan {
+    uint32_t samples_per_chunk;
+    uint32_t n_big;         /* full chunks per pixel */
+    uint32_t tail_samples;  /* samples of the halving tail (0: none) */
+    uint32_t n_tail;        /* chunks of the tail */
+    uint32_t n_chunks;      /* n_big + n_tail */
+    uint32_t n_local_px;    /* pixels of the rank's tile slab (padding included) */
+    uint64_t n_items;       /* work items = n_chunks * n_local_px */
+    uint32_t cus;           /* compute units the plan assumed */
+    uint32_t pad;
+} rtow_plan;
+int rtow_render_plan(const rtow_context* ctx, const rtow_params* p, rtow_plan* out);
+
 /* Drop-in for main.cpp:932-996 on one GPU: render every pixel, write the BGRA
  * frame (host memory, W*H*4, alpha 0) and, if linear_out is not NULL, the
  * averaged linear RGB before sqrt/quantise (W*H*3 floats, same pixel order).
@@ -383,6 +405,46 @@ int rtow_debug_trace_sample(rtow_context* ctx, const rtow_camera* cam, const rto
 int rtow_assemble_device(rtow_context* ctx, uint32_t width, uint32_t height, uint32_t world,
                          const void* d_slabs, uint32_t slab_stride_px, void* d_bgra_frame,
                          void* stream);
+/* The same for gathered LINEAR slabs (3 floats per pixel) into a device
+ * W*H*3 float frame. */
+int rtow_assemble_linear_device(rtow_context* ctx, uint32_t width, uint32_t height, uint32_t world,
+                                const void* d_slabs, uint32_t slab_stride_px, void* d_linear_frame,
+                                void* stream);
+
+/* ---- several GPUs from one process -------------------------------------------
+ * The reference renders a frame with N std::threads over one shared buffer,
+ * thread i taking columns i, i+N, ... (main.cpp:182-195, 936).  rtow_multi is
+ * that split across GPUs, for a caller that is one process (main.cpp):
+ *   - one rtow_context per device (its stream, scene copy and buffers);
+ *   - device i renders rank i of world n: the 8x8 tiles i, i+n, ... into a
+ *     compact slab (rtow_render_tiles_device), all devices at once;
+ *   - one RCCL gather: communicators from ncclCommInitAll over `devices`, the
+ *     slabs sent to device 0 with grouped ncclSend / ncclRecv over xGMI (RCCL
+ *     has no gather primitive); device 0's slab goes through RCCL too;
+ *   - device 0 assembles the BGRA frame (and the linear one) and copies it out.
+ * The frame equals rtow_render's bit for bit for any n: the RNG is keyed by
+ * global pixel and sample, and the pixel sums are exact.  HIP failures return
+ * RTOW_E_HIP, RCCL failures RTOW_E_RCCL (ncclResult text in rtow_last_error).
+ * `devices`: n distinct HIP device indices, device 0 of the list gathers. */
+typedef struct rtow_multi rtow_multi;
+int rtow_multi_create(const int* devices, uint32_t n_devices, rtow_multi** out);
+int rtow_multi_destroy(rtow_multi* m);
+uint32_t rtow_multi_device_count(const rtow_multi* m);
+/* rtow_context_set_tree on every device (before rtow_multi_upload). */
+int rtow_multi_set_tree(rtow_multi* m, int tree);
+/* rtow_scene_upload on every device (the scene is replicated: <= ~10 MB). */
+int rtow_multi_upload(rtow_multi* m, const rtow_scene* scene);
+/* One frame over all devices (p->rank / p->world are ignored: device i is rank
+ * i of n).  bgra_out: host W*H*4 (may be NULL); linear_out: host W*H*3 floats
+ * (may be NULL).  stats: whole call -- segments / samples / pixels summed,
+ * kernel_ms and resolve_ms the slowest device's, total_ms the wall clock
+ * including the gather and assembly.  device_stats (may be NULL): n entries,
+ * each device's own. */
+int rtow_multi_render(rtow_multi* m, const rtow_camera* cam, const rtow_params* p, uint8_t* bgra_out,
+                      float* linear_out, rtow_stats* stats, rtow_stats* device_stats);
+/* create + upload + render + destroy in one call. */
+int rtow_render_devices(const int* devices, uint32_t n_devices, const rtow_scene* scene, const rtow_camera* cam,
+                        const rtow_params* p, uint8_t* bgra_out, float* linear_out, rtow_stats* stats);
 
 #ifdef __cplusplus
 }

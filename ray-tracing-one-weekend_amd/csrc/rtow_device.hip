@@ -81,6 +81,57 @@ __device__ __forceinline__ F3 unit(F3 v) {
     return divs(v, l);
 }
 __device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]); }
+
+// Scene records read through the constant address space: the scene is
+// read-only for a kernel's lifetime, and a load whose address is uniform
+// across the wave (the top-level scan's items, their instance chains, Box
+// corners, media: every lane is on the same item) then becomes a scalar
+// s_load into SGPRs through the scalar cache, used directly as VALU operands,
+// instead of a 64-lane vector load through the vector L1 (the general
+// kernels' waves wait ~45 % of their cycles, mostly on vector memory).  A
+// divergent address still compiles to a vector load.  RTOW_SCALAR=0 reads
+// them as plain global loads (A/B).
+#ifndef RTOW_SCALAR
+#define RTOW_SCALAR 1
+#endif
+#define RTOW_CONST_AS __attribute__((address_space(4)))
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));  // 16-B aligned: a divergent load stays one dwordx4
+template <class T>
+__device__ __forceinline__ T cld(const T* p) {
+#if RTOW_SCALAR
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    uint32_t w[sizeof(T) / 4];
+    if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
+        const RTOW_CONST_AS u32x4_t* q = (const RTOW_CONST_AS u32x4_t*)p;
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(T) / 16); i++) {
+            const u32x4_t v = q[i];
+            w[4 * i] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+    } else {
+        const RTOW_CONST_AS uint32_t* q = (const RTOW_CONST_AS uint32_t*)p;
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(T) / 4); i++) w[i] = q[i];
+    }
+    T out;
+    __builtin_memcpy(&out, w, sizeof(T));
+    return out;
+#else
+    return *p;
+#endif
+}
+// 16 bytes at a 16-B aligned address
+__device__ __forceinline__ float4 cld4(const void* p) {
+#if RTOW_SCALAR
+    const u32x4_t v = *(const RTOW_CONST_AS u32x4_t*)p;
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+#else
+    return *reinterpret_cast<const float4*>(p);
+#endif
+}
 __device__ __forceinline__ float comp(F3 v, uint32_t i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 
 struct Ray {
@@ -129,7 +180,7 @@ struct DevParams {
     // the DBG kernel records (RTOW_DEBUG_SEG_FLOATS floats each) into dbg_out
     uint32_t dbg_col, dbg_row, dbg_sample, dbg_max;
     float* dbg_out;
-    struct XFrame* xframes;  // xhit's call frames: XDEPTH x xstride (the grid's threads)
+    struct XFrame* xframes;  // xhit's call frames: DevScene::xdepth x xstride (the grid's threads)
     uint32_t xstride;
 };
 
@@ -168,11 +219,11 @@ __device__ __forceinline__ Ray root_ray(const DevScene& S, const Ray& w) {
 
 // the ray in the frame of chain `id` (DevScene::chains), outermost first
 __device__ __forceinline__ Ray chain_ray(const DevScene& S, uint32_t id, const Ray& w) {
-    const DChainX& C = S.chains[id];
-    const int n = (int)C.n;
+    const DChainX* C = S.chains + id;
+    const int n = (int)cld(&C->n);
     Ray r = w;
     for (int k = 0; k < n; k++) {
-        const float4 e = C.t[k];
+        const float4 e = cld4(C->t + k);
         const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
         if (kind == DK_TRANSLATE) {
             r.o = sub(r.o, f3(e.y, e.z, e.w));
@@ -193,9 +244,9 @@ __device__ __forceinline__ void inst_out(const DevScene& S, uint32_t ref, F3& p,
 
 // the way out of the instances, innermost first
 __device__ __forceinline__ void chain_out(const DevScene& S, uint32_t id, F3& p, F3& nrm) {
-    const DChainX& C = S.chains[id];
-    for (int k = (int)C.n - 1; k >= 0; k--) {  // inst_out's operations
-        const float4 e = C.t[k];
+    const DChainX* C = S.chains + id;
+    for (int k = (int)cld(&C->n) - 1; k >= 0; k--) {  // inst_out's operations
+        const float4 e = cld4(C->t + k);
         const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
         if (kind == DK_FLIP) {
             nrm = neg(nrm);
@@ -337,17 +388,17 @@ struct Sph {
 };
 
 __device__ __forceinline__ Sph load_sph(const DSphere* p) {
-    const float4 a = reinterpret_cast<const float4*>(p)[0];
-    const float4 b = reinterpret_cast<const float4*>(p)[1];
-    const uint4 c = reinterpret_cast<const uint4*>(p)[2];
+    const float4 a = cld4(p);
+    const float4 b = cld4(reinterpret_cast<const float4*>(p) + 1);
+    const float4 c = cld4(reinterpret_cast<const float4*>(p) + 2);
     Sph s;
     s.c0 = f3(a.x, a.y, a.z);
     s.r = a.w;
     s.dc = f3(b.x, b.y, b.z);
     s.t0 = b.w;
-    s.t1 = __uint_as_float(c.x);
-    s.mat = c.y;
-    s.moving = c.z;
+    s.t1 = c.x;
+    s.mat = __float_as_uint(c.y);
+    s.moving = __float_as_uint(c.z);
     return s;
 }
 
@@ -618,8 +669,8 @@ __device__ __forceinline__ void box6_side(const DevScene& S, float a0, float a1,
 }
 __device__ __forceinline__ bool box6_scan(const DevScene& S, uint32_t bi, const Ray& r, const F3& inv, float tmin,
                                           float& bt, uint32_t& best) {
-    const float4 lo = reinterpret_cast<const float4*>(S.box6 + bi)[0];
-    const float4 hi = reinterpret_cast<const float4*>(S.box6 + bi)[1];
+    const float4 lo = cld4(S.box6 + bi);
+    const float4 hi = cld4(reinterpret_cast<const float4*>(S.box6 + bi) + 1);
     const uint32_t f = __float_as_uint(lo.w);
     bool found = false;
     box6_side<2, 0, 1>(S, lo.x, hi.x, lo.y, hi.y, hi.z, f + 0, r, inv, tmin, bt, best, found);  // XY at z1 (flipped)
@@ -634,8 +685,8 @@ __device__ __forceinline__ bool box6_scan(const DevScene& S, uint32_t bi, const 
 // in [lo_t, near] (which side does not matter), near shrinking as sides hit
 __device__ __forceinline__ bool box6_nearest(const DevScene& S, uint32_t bi, const Ray& r, const F3& inv, float lo_t,
                                              float& near) {
-    const float4 lo = reinterpret_cast<const float4*>(S.box6 + bi)[0];
-    const float4 hi = reinterpret_cast<const float4*>(S.box6 + bi)[1];
+    const float4 lo = cld4(S.box6 + bi);
+    const float4 hi = cld4(reinterpret_cast<const float4*>(S.box6 + bi) + 1);
     bool f = false;
     float t;
     if (rect_t_ax<2, 0, 1>(lo.x, hi.x, lo.y, hi.y, hi.z, r, inv, lo_t, near, t)) near = t, f = true;
@@ -1039,7 +1090,7 @@ template <int STACK, bool ANYB>
 __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, const Ray& r, float a, float ra,
                                            const Ray& wray, float tmin, float& bt, uint32_t* stk, int sp, Rng& rng,
                                            uint32_t& overflow) {
-    const DMedium M = S.med[idx];
+    const DMedium M = cld(S.med + idx);
     (void)rng.next();  // the discarded `db` draw (constantMedium.h:27)
     float t1 = 0, t2 = 0;
     bool two = false;
@@ -1072,7 +1123,7 @@ __device__ __forceinline__ bool medium_hit(const DevScene& S, uint32_t idx, cons
             float near = FLT_MAX, t;
             bool f = false;
             for (uint32_t k = 0; k < M.bcount; k++) {
-                if (rect_t(S.rect[M.bfirst + k], rb, inv, lo, near, t)) {
+                if (rect_t(cld(S.rect + M.bfirst + k), rb, inv, lo, near, t)) {
                     near = t;
                     f = true;
                 }
@@ -1312,7 +1363,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             if (j < 8 && first_active_lane()) prof->visits_item[j]++;
             t0 = t1;
         }
-        const DTop T = S.n_top ? S.top[j] : DTop{TOP_GENERIC, S.root, 0, 0};
+        const DTop T = S.n_top ? cld(S.top + j) : DTop{TOP_GENERIC, S.root, 0, 0};
         const uint32_t kind = T.kind & TOP_KIND_MASK;
         if (kind == TOP_GENERIC) {  // (media too: traverse() keeps their draws in order)
             // the scan's ray is dead across the general traversal (the host
@@ -1348,7 +1399,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         } else if (kind == TOP_RECTS) {
             for (uint32_t k = 0; k < T.b; k++) {
                 float t;
-                if (rect_t(S.rect[T.a + k], r, inv, tmin, bt, t)) take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k));
+                if (rect_t(cld(S.rect + T.a + k), r, inv, tmin, bt, t)) take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k));
             }
         } else if (TOPMED && kind == TOP_MEDIUM) {
             // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
@@ -1524,8 +1575,9 @@ __device__ __forceinline__ bool xhit(const DevScene& S, const DevParams& P, cons
     rr.t = rr.u = rr.v = 0.0f;
     rr.p = rr.n = f3(0, 0, 0);
     rr.mat = 0;
+    const int maxd = (int)S.xdepth;  // the world's deepest hit() recursion (rawDepth): the frames allocated
     auto call = [&](uint32_t h, const Ray& r, float t0, float t1) {
-        if (d >= XDEPTH) {
+        if (d >= maxd) {
             overflow = 1;
             rh = false;
             return;
@@ -2494,6 +2546,20 @@ __global__ void assemble_kernel(uint32_t W, uint32_t H, uint32_t world, uint32_t
     fb[i] = slabs[(size_t)rank * stride_px + slot * 64u + (y & 7u) * 8u + (x & 7u)];
 }
 
+// the same for linear slabs: 3 floats per pixel
+__global__ void assemble_lin_kernel(uint32_t W, uint32_t H, uint32_t world, uint32_t tiles_x, const float* slabs,
+                                    uint32_t stride_px, float* fb) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W * H) return;
+    const uint32_t x = i % W, y = i / W;
+    const uint32_t tile = (y >> 3) * tiles_x + (x >> 3);
+    const uint32_t rank = tile % world, slot = tile / world;
+    const float* s = slabs + 3 * ((size_t)rank * stride_px + slot * 64u + (y & 7u) * 8u + (x & 7u));
+    fb[3 * (size_t)i] = s[0];
+    fb[3 * (size_t)i + 1] = s[1];
+    fb[3 * (size_t)i + 2] = s[2];
+}
+
 #endif  // host translation unit
 
 // Every trace_kernel instantiation the host launches (launchWaves), listed
@@ -2607,6 +2673,7 @@ struct HostLayout {
     std::vector<XHit> xh;
     std::vector<uint32_t> xrefs;
     uint32_t xroot = 0;
+    uint32_t xdepth = 0;  // rawDepth of the raw graph (general and exact worlds): xhit's frames per thread
 };
 
 // The deepest hit() recursion the reference runs over the raw graph (xhit's
@@ -2661,6 +2728,7 @@ int buildExact(const rtow_scene& s, HostLayout& L) {
     std::memcpy(L.xh.data(), s.hitables, sizeof(XHit) * s.n_hitables);
     L.xrefs.assign(s.refs, s.refs + s.n_refs);
     L.xroot = s.root;
+    L.xdepth = depth;
     L.stack_need = depth;
     return RTOW_OK;
 }
@@ -4209,7 +4277,8 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
         // the raw graph, for the rays whose record only the reference's own
         // recursion settles (xhit after ref_skips_hit / tie_unsettled)
         std::vector<int> memo(s.n_hitables, 0);
-        if (rawDepth(s, s.root, memo) > (uint32_t)XDEPTH)
+        L.xdepth = rawDepth(s, s.root, memo);
+        if (L.xdepth > (uint32_t)XDEPTH)
             return set_error(RTOW_E_UNSUPPORTED, "scene graph deeper than " + std::to_string(XDEPTH) + " calls (or cyclic)");
         L.xh.resize(s.n_hitables);
         std::memcpy(L.xh.data(), s.hitables, sizeof(XHit) * s.n_hitables);
@@ -4315,14 +4384,17 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
         }
     }
     if (occ < 1) occ = 1;
-    uint32_t per = bpc ? bpc : (uint32_t)occ;
+    // a persistent grid gains nothing from blocks that cannot be resident:
+    // blocks_per_cu is capped at the occupancy (it also sizes xhit's frames)
+    uint32_t per = bpc ? std::min(bpc, (uint32_t)occ) : (uint32_t)occ;
     uint32_t grid = (uint32_t)c->cus * per;
     uint32_t maxUseful = (P.n_items + BS - 1) / BS;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
     DevParams Pk = P;
-    if constexpr (MODE != 0) {  // xhit's call frames, one column per grid thread
+    if constexpr (MODE != 0) {  // xhit's call frames, one column per grid thread, as deep as the world's recursion
         Pk.xstride = grid * (uint32_t)BS;
-        const int rc = ensure((void**)&c->d_xframes, &c->xframes_bytes, (size_t)Pk.xstride * XDEPTH * sizeof(XFrame));
+        const int rc = ensure((void**)&c->d_xframes, &c->xframes_bytes,
+                              (size_t)Pk.xstride * c->scene.xdepth * sizeof(XFrame));
         if (rc) return rc;
         Pk.xframes = (XFrame*)c->d_xframes;
     }
@@ -4377,7 +4449,9 @@ int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32
     return launchStack<3>(c, cam, P, bpc, st);
 }
 
-int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
+// cus: the device's compute units (the automatic chunk length depends on the
+// grid); auto_spc: RTOW_AUTO_SPC (0: none)
+int planParams(int cus, uint32_t auto_spc, const rtow_params* p, DevParams& P) {
     if (!p || p->width == 0 || p->height == 0 || p->spp == 0) return set_error(RTOW_E_INVALID, "bad params");
     if ((uint64_t)p->width * p->height > (1ull << 31) || p->width > (1u << 24) || p->height > (1u << 24))
         return set_error(RTOW_E_INVALID, "image too large");
@@ -4399,9 +4473,9 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     // RTOW_AUTO_SPC (c->auto_spc) fixes the length instead.
     const uint32_t n_px = rtow_rank_tile_count(p->width, p->height, p->rank, world) * 64u;
     uint32_t spc = p->samples_per_chunk;
-    if (!spc && c->auto_spc) spc = c->auto_spc;
+    if (!spc && auto_spc) spc = auto_spc;
     if (!spc) {
-        const uint64_t lanes = (uint64_t)std::max(1, c->cus) * 1024u;
+        const uint64_t lanes = (uint64_t)std::max(1, cus) * 1024u;
         spc = 16;
         for (uint32_t cand : {128u, 64u, 32u}) {
             if ((uint64_t)n_px * ((p->spp + cand - 1) / cand) >= 30 * lanes) {
@@ -4439,6 +4513,12 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     P.sky_gain = p->sky_gain;
     P.gi_gain = p->gi_gain;
     P.seed = p->seed;
+    return RTOW_OK;
+}
+
+int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
+    const int rc = planParams(c->cus, c->auto_spc, p, P);
+    if (rc) return rc;
     P.dbg_out = c->dbg_out;
     P.dbg_col = c->dbg_col;
     P.dbg_row = c->dbg_row;
@@ -4649,6 +4729,23 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
     return RTOW_OK;
 }
 
+int rtow_render_plan(const rtow_context* c, const rtow_params* p, rtow_plan* out) {
+    if (!p || !out) return set_error(RTOW_E_INVALID, "NULL argument");
+    const int cus = c ? c->cus : 256;  // MI355X: 256 CUs
+    DevParams P;
+    const int rc = planParams(cus, c ? c->auto_spc : 0u, p, P);
+    if (rc) return rc;
+    out->samples_per_chunk = P.spc;
+    out->n_big = P.n_big;
+    out->tail_samples = P.n_tail ? P.tail_r : 0u;
+    out->n_tail = P.n_tail;
+    out->n_chunks = P.n_chunks;
+    out->n_local_px = P.n_local_px;
+    out->n_items = P.n_items;
+    out->cus = (uint32_t)cus;
+    return RTOW_OK;
+}
+
 int rtow_context_set_tree(rtow_context* c, int tree) {
     if (!c) return set_error(RTOW_E_INVALID, "NULL context");
     if (tree != RTOW_TREE_SAH && tree != RTOW_TREE_REFERENCE) return set_error(RTOW_E_INVALID, "unknown tree");
@@ -4753,6 +4850,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.xrefs = (const uint32_t*)(b + o_xrefs);
     d.xroot = L.xroot;
     d.exact = L.exact ? 1u : 0u;
+    d.xdepth = std::max(1u, L.xdepth);
     c->has_scene = true;
     // progressive sums belong to the scene they were rendered from: a new
     // scene restarts them (rtow_render_progressive)
@@ -4907,6 +5005,23 @@ int rtow_assemble_device(rtow_context* c, uint32_t width, uint32_t height, uint3
     const uint32_t n = width * height;
     hipLaunchKernelGGL(assemble_kernel, dim3((n + 255) / 256), dim3(256), 0, st, width, height, world, (width + 7) / 8,
                        (const uint32_t*)d_slabs, slab_stride_px, (uint32_t*)d_bgra_frame);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    return RTOW_OK;
+}
+
+int rtow_assemble_linear_device(rtow_context* c, uint32_t width, uint32_t height, uint32_t world,
+                                const void* d_slabs, uint32_t slab_stride_px, void* d_linear_frame, void* stream) {
+    if (!c || !d_slabs || !d_linear_frame || width == 0 || height == 0)
+        return set_error(RTOW_E_INVALID, "bad arguments");
+    if (world == 0) world = 1;
+    if (slab_stride_px < rtow_rank_tile_count(width, height, 0, world) * 64u)
+        return set_error(RTOW_E_INVALID, "slab stride smaller than rank 0's slab");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIP_TRY(hipSetDevice(c->device));
+    const uint32_t n = width * height;
+    hipLaunchKernelGGL(assemble_lin_kernel, dim3((n + 255) / 256), dim3(256), 0, st, width, height, world,
+                       (width + 7) / 8, (const float*)d_slabs, slab_stride_px, (float*)d_linear_frame);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
     return RTOW_OK;

@@ -275,6 +275,7 @@ struct DevScene {
     const uint32_t* xrefs;
     uint32_t xroot;
     uint32_t exact;
+    uint32_t xdepth;  // the deepest hit() recursion of the raw graph (rawDepth, <= XDEPTH): xhit's frames per thread
 };
 
 // One reference Hitable, as rtow_hitable (include/rtow.h) lays it out.

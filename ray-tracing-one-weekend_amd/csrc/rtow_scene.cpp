@@ -677,6 +677,7 @@ const char* rtow_error_string(int code) {
     case RTOW_E_NO_DEVICE: return "no GPU device";
     case RTOW_E_IO: return "I/O error";
     case RTOW_E_NOMEM: return "out of memory";
+    case RTOW_E_RCCL: return "RCCL error";
     default: return "unknown error";
     }
 }

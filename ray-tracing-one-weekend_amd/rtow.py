@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("RTOW_LIB") or os.path.join(PKG_DIR, "librtow_hip.so")
 HEADER = os.path.join(REPO, "include", "rtow.h")
 
 # ---- constants (include/rtow.h) ---------------------------------------------
-OK, E_INVALID, E_UNSUPPORTED, E_HIP, E_NO_DEVICE, E_IO, E_NOMEM = 0, -1, -2, -3, -4, -5, -6
+OK, E_INVALID, E_UNSUPPORTED, E_HIP, E_NO_DEVICE, E_IO, E_NOMEM, E_RCCL = 0, -1, -2, -3, -4, -5, -6, -7
 SCENE_THREE_SPHERE, SCENE_RANDOM_NED, SCENE_CORNELL_NED, SCENE_CORNELL_SMOKE = 1, 2, 3, 4
 SCENE_FINAL_NED = 5
 SCENES = {"three_sphere": SCENE_THREE_SPHERE, "random_ned": SCENE_RANDOM_NED, "cornell": SCENE_CORNELL_NED,
@@ -56,6 +56,16 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Plan(ctypes.Structure):
+    _fields_ = [("samples_per_chunk", ctypes.c_uint32), ("n_big", ctypes.c_uint32),
+                ("tail_samples", ctypes.c_uint32), ("n_tail", ctypes.c_uint32), ("n_chunks", ctypes.c_uint32),
+                ("n_local_px", ctypes.c_uint32), ("n_items", ctypes.c_uint64), ("cus", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
 
 
 class BuildOpts(ctypes.Structure):
@@ -108,6 +118,7 @@ def lib():
         "rtow_context_destroy": ([vp], i32),
         "rtow_scene_upload": ([vp, vp], i32),
         "rtow_context_set_tree": ([vp, i32], i32),
+        "rtow_render_plan": ([vp, ctypes.POINTER(Params), ctypes.POINTER(Plan)], i32),
         "rtow_debug_trace_sample": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), u32, u32, u32, vp, u32,
                                      ctypes.POINTER(u32)], i32),
         "rtow_write_bmp": ([ctypes.c_char_p, vp, ctypes.c_uint64, u32, u32, u32], i32),
@@ -118,6 +129,16 @@ def lib():
         "rtow_render_progressive_tiles_device": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), i32, vp, vp,
                                                   vp, ctypes.POINTER(u32), ctypes.POINTER(Stats)], i32),
         "rtow_assemble_device": ([vp, u32, u32, u32, vp, u32, vp, vp], i32),
+        "rtow_assemble_linear_device": ([vp, u32, u32, u32, vp, u32, vp, vp], i32),
+        "rtow_multi_create": ([ctypes.POINTER(i32), u32, ctypes.POINTER(vp)], i32),
+        "rtow_multi_destroy": ([vp], i32),
+        "rtow_multi_device_count": ([vp], u32),
+        "rtow_multi_set_tree": ([vp, i32], i32),
+        "rtow_multi_upload": ([vp, vp], i32),
+        "rtow_multi_render": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats),
+                               vp], i32),
+        "rtow_render_devices": ([ctypes.POINTER(i32), u32, vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), vp, vp,
+                                 ctypes.POINTER(Stats)], i32),
         "rtow_image_decode_jpeg": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp), ctypes.POINTER(u32),
                                     ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
         "rtow_image_load_jpeg": ([ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(u32), ctypes.POINTER(u32),
@@ -225,6 +246,15 @@ def camera_oriented(width, height, look_from, rows):
     c = Camera()
     check(lib().rtow_camera_oriented(width, height, lf, rw, ctypes.byref(c)), "rtow_camera_oriented")
     return c
+
+
+def plan(p, ctx=None):
+    """rtow_render_plan: how a render with params `p` cuts its work items (ctx
+    None: a 256-CU MI355X)."""
+    out = Plan()
+    check(lib().rtow_render_plan(ctx._h if ctx is not None else None, ctypes.byref(p), ctypes.byref(out)),
+          "rtow_render_plan")
+    return out
 
 
 def tile_count(width, height):
@@ -402,9 +432,52 @@ class Context:
         check(lib().rtow_assemble_device(self._h, width, height, world, d_slabs, stride_px, d_frame, stream),
               "rtow_assemble_device")
 
+    def assemble_linear_device(self, width, height, world, d_slabs, stride_px, d_frame, stream=None):
+        check(lib().rtow_assemble_linear_device(self._h, width, height, world, d_slabs, stride_px, d_frame, stream),
+              "rtow_assemble_linear_device")
+
     def close(self):
         if self._h:
             lib().rtow_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Multi:
+    """rtow_multi: several GPUs from one process (device i renders rank i of n,
+    one RCCL gather to the first device, which assembles the frame)."""
+
+    def __init__(self, devices):
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        check(lib().rtow_multi_create(devs, len(devices), ctypes.byref(h)), "rtow_multi_create")
+        self._h = h
+        self.n = len(devices)
+
+    def set_tree(self, tree):
+        check(lib().rtow_multi_set_tree(self._h, TREES[tree]), "rtow_multi_set_tree")
+
+    def upload(self, scene):
+        check(lib().rtow_multi_upload(self._h, scene.view_ptr), "rtow_multi_upload")
+
+    def render(self, cam, p, linear=True):
+        """(bgra[H,W,4], linear[H,W,3] or None, Stats, [per-device Stats])."""
+        bgra = np.zeros((p.height, p.width, 4), np.uint8)
+        lin = np.zeros((p.height, p.width, 3), np.float32) if linear else None
+        st = Stats()
+        dst = (Stats * self.n)()
+        check(lib().rtow_multi_render(self._h, ctypes.byref(cam), ctypes.byref(p), bgra.ctypes.data,
+                                      lin.ctypes.data if linear else None, ctypes.byref(st), dst), "rtow_multi_render")
+        return bgra, lin, st, list(dst)
+
+    def close(self):
+        if self._h:
+            lib().rtow_multi_destroy(self._h)
             self._h = None
 
     def __del__(self):

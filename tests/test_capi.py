@@ -19,7 +19,7 @@ def test_exports_every_declared_symbol():
 def test_abi_version_and_errors():
     L = rtow.lib()
     assert L.rtow_abi_version() == 1
-    for code in range(-6, 1):
+    for code in range(-7, 1):
         assert L.rtow_error_string(code)
     assert L.rtow_error_string(-99) == b"unknown error"
 
@@ -49,6 +49,60 @@ def test_bad_arguments_fail_loudly():
         rtow.Scene.build("random_ned", n=2)
 
 
+@pytest.mark.parametrize("W,H,spp,rank,world,spc,n_big,tail,n_tail", [
+    (1920, 1080, 1024, 0, 1, 128, 7, 128, 8),   # the bench's config-2 frame on one GPU
+    (1920, 1080, 1024, 0, 2, 128, 7, 128, 8),
+    (1920, 1080, 1024, 0, 4, 64, 15, 64, 7),
+    (1920, 1080, 1024, 3, 8, 32, 31, 32, 6),    # one rank of the 8-GPU config-2 frame
+    (4096, 4096, 8192, 0, 8, 128, 63, 128, 8),  # config 5: rank 0 of 8
+    (4096, 4096, 512, 0, 8, 128, 3, 128, 8),    # the config-5 share the GPU parity test renders
+    (800, 800, 4096, 0, 1, 128, 31, 128, 8),    # configs 3/4
+    (64, 36, 16, 0, 1, 16, 1, 0, 0),            # small frames: one 16-sample chunk, no tail
+])
+def test_render_plan_matches_the_documented_chunking(W, H, spp, rank, world, spc, n_big, tail, n_tail):
+    """rtow_render_plan (no context: a 256-CU MI355X) exposes the automatic
+    chunking the kernels run: 128/64/32/16-sample items leaving >= 30 items per
+    lane, then the halving tail (DevParams, rtow_device.hip)."""
+    pl = rtow.plan(rtow.params(W, H, spp, rank=rank, world=world))
+    assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail) == (spc, n_big, tail, n_tail)
+    assert pl.n_chunks == n_big + n_tail and pl.cus == 256
+    assert pl.n_local_px == rtow.rank_tile_count(W, H, rank, world) * 64
+    assert pl.n_items == pl.n_chunks * pl.n_local_px
+    # the chunks cover every sample once: n_big full chunks, then the tail
+    assert n_big * spc + tail == spp or (n_tail == 0 and (n_big - 1) * spc < spp <= n_big * spc)
+    fixed = rtow.plan(rtow.params(W, H, spp, rank=rank, world=world, samples_per_chunk=16))
+    assert (fixed.samples_per_chunk, fixed.n_tail) == (16, 0) and fixed.n_big == (spp + 15) // 16
+    with pytest.raises(rtow.RtowError):
+        rtow.plan(rtow.params(W, H, 0))
+
+
 def test_device_count_without_gpu_is_not_a_crash():
     # here (no GPU) this returns 0; on the GPU box >= 1
     assert rtow.device_count() >= 0
+
+
+def test_multi_gpu_arguments_are_validated_before_any_gpu_call():
+    """rtow_multi_create / rtow_render_devices (several GPUs from one process,
+    one RCCL gather): bad device lists fail with E_INVALID before HIP or RCCL
+    is touched; a valid list on a machine without a GPU is E_NO_DEVICE."""
+    L = rtow.lib()
+    h = ctypes.c_void_p()
+    i32 = ctypes.c_int
+    assert L.rtow_multi_create(None, 1, ctypes.byref(h)) == rtow.E_INVALID
+    assert L.rtow_multi_create((i32 * 1)(0), 0, ctypes.byref(h)) == rtow.E_INVALID
+    assert L.rtow_multi_create((i32 * 2)(0, 0), 2, ctypes.byref(h)) == rtow.E_INVALID  # listed twice
+    assert b"twice" in L.rtow_last_error()
+    assert L.rtow_multi_create((i32 * 2)(0, -1), 2, ctypes.byref(h)) == rtow.E_INVALID
+    assert L.rtow_multi_create((i32 * 1)(0), 1, None) == rtow.E_INVALID
+    assert h.value is None
+    assert L.rtow_multi_destroy(None) == rtow.OK
+    assert L.rtow_multi_device_count(None) == 0
+    assert L.rtow_multi_upload(None, None) == rtow.E_INVALID
+    assert L.rtow_multi_render(None, None, None, None, None, None, None) == rtow.E_INVALID
+    cam, p = rtow.camera_main(16, 8), rtow.params(16, 8, 1)
+    assert L.rtow_render_devices((i32 * 1)(0), 1, None, ctypes.byref(cam), ctypes.byref(p), None, None,
+                                 None) == rtow.E_INVALID
+    if rtow.device_count() == 0:
+        rc = L.rtow_multi_create((i32 * 2)(0, 1), 2, ctypes.byref(h))
+        assert rc == rtow.E_NO_DEVICE and h.value is None
+    assert L.rtow_error_string(rtow.E_RCCL) == b"RCCL error"

@@ -1,0 +1,94 @@
+"""Parity on the exact path bench.py times ("Pin parity on the
+benched path").
+
+The bench renders config 2 at 1920x1080x1024 spp through
+rtow_render_tiles_device (rank 0 of 1) with automatic chunking: 128-sample work
+items (seven per pixel) and a halving tail of 64/32/16/8/4/2/1/1 samples, each
+chunk summed in float in sample order (main.cpp:939-946) and added to the
+pixel's fixed-point sum.  Config 5 is quoted for 8 GPUs; one rank's share of
+its 4096x4096 frame also runs on 128-sample items.  These tests render those
+exact launches and compare a random pixel sample with the C oracle (the
+reference's recursion, main.cpp:939-955 / color.h:12-59) at the same spp.
+
+Bar: per-channel RMS <= 1e-4 (BASELINE north_star) and at most 1 pixel per
+10^5 off by more than 1e-3.
+"""
+import numpy as np
+import pytest
+
+import rtow
+import scene_io as sio
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-4
+
+
+def _slab_render(ctx, scene, W, H, spp, seed, rank, world):
+    """One rtow_render_tiles_device launch (bench.py's HipRank.step) with a
+    linear slab; returns (linear frame values of the rank's pixels keyed by
+    framebuffer index, stats, plan)."""
+    import torch
+
+    ctx.upload(scene)
+    cam = rtow.camera_main(W, H)
+    p = rtow.params(W, H, spp, seed=seed, rank=rank, world=world)
+    stride = rtow.rank_tile_count(W, H, rank, world) * 64
+    bgra = torch.zeros(stride * 4, dtype=torch.uint8, device="cuda")
+    lin = torch.zeros(stride * 3, dtype=torch.float32, device="cuda")
+    st = ctx.render_tiles_device(cam, p, bgra.data_ptr(), lin.data_ptr())
+    torch.cuda.synchronize()
+    idx = rtow.rank_pixels(W, H, rank, world)
+    return cam, p, idx, lin.cpu().numpy().reshape(-1, 3), st, rtow.plan(p, ctx)
+
+
+def _compare(scene, cam, p, idx, lin, n_pix, seed):
+    ok = np.flatnonzero(idx >= 0)
+    rng = np.random.default_rng(seed)
+    pick = rng.choice(ok, size=n_pix, replace=False)
+    pix = idx[pick].astype(np.uint32)
+    olin, _, oc = sio.oracle_render(scene.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p)), pixels=pix, threads=16)
+    g = lin[pick].astype(np.float64)
+    d = np.abs(g - olin).max(axis=1)
+    rms = np.sqrt(np.mean((g - olin) ** 2, axis=0))
+    return rms, d, oc
+
+
+def test_config2_bench_frame_1024spp(gpu_ctx):
+    """Config 2 exactly as benched: randomScene_NED n=487, 1920x1080x1024,
+    seed 1, one rank, automatic chunking (128-sample items, n_big 7, a
+    128-sample halving tail in 8 chunks); 3000 random pixels vs the oracle."""
+    W, H, spp = 1920, 1080, 1024
+    scene = rtow.Scene.build("random_ned", n=487, image="synthetic", scene_seed=1)
+    cam, p, idx, lin, st, pl = _slab_render(gpu_ctx, scene, W, H, spp, 1, 0, 1)
+    assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail) == (128, 7, 128, 8), pl.as_dict()
+    assert st.samples == W * H * spp
+    rms, d, oc = _compare(scene, cam, p, idx, lin, 3000, 0)
+    n_off = int((d > 1e-3).sum())
+    print(f"BENCHED config2 1920x1080x1024: plan {pl.as_dict()} rms {rms} max|d| {d.max():.3g} "
+          f"pixels>1e-3 {n_off}/3000 bit-identical {float(np.mean(d == 0)):.4f} "
+          f"rays/sample gpu {st.segments / st.samples:.4f} oracle-sample {oc.segments / oc.samples:.4f} "
+          f"kernel {st.kernel_ms:.1f} ms")
+    assert np.isfinite(lin).all()
+    assert (rms <= RMS_TOL).all(), rms
+    assert n_off <= int(1e-5 * 3000)
+
+
+def test_config5_rank_share_128_sample_items(gpu_ctx):
+    """Config 5's 8-GPU split: rank 0's share of final_ned 4096x4096 at 512 spp,
+    which picks 128-sample items (n_big 3 + the 128-sample tail) as the 8192-spp
+    bench share does (n_big 63); 500 random pixels of the slab vs the oracle."""
+    W, H, spp = 4096, 4096, 512
+    scene = rtow.Scene.build("final_ned", n=1, image="synthetic", scene_seed=1)
+    cam, p, idx, lin, st, pl = _slab_render(gpu_ctx, scene, W, H, spp, 1, 0, 8)
+    assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail) == (128, 3, 128, 8), pl.as_dict()
+    full = rtow.plan(rtow.params(W, H, 8192, rank=0, world=8), gpu_ctx)
+    assert (full.samples_per_chunk, full.n_big, full.n_tail) == (128, 63, 8)
+    rms, d, oc = _compare(scene, cam, p, idx, lin, 500, 1)
+    n_off = int((d > 1e-3).sum())
+    print(f"BENCHED config5 share 0/8 4096^2x512: plan {pl.as_dict()} rms {rms} max|d| {d.max():.3g} "
+          f"pixels>1e-3 {n_off}/500 bit-identical {float(np.mean(d == 0)):.4f} kernel {st.kernel_ms:.1f} ms")
+    assert np.isfinite(lin).all()
+    assert (rms <= RMS_TOL).all(), rms
+    assert n_off <= int(1e-5 * 500)
