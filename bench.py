@@ -435,7 +435,8 @@ def run(args, make_rank):
         scene, _, W0, H0, spp0, label = WORKLOADS[args.workload]
         W, H, spp = args.width, args.height, args.spp
         is_baseline_cfg = args.workload == "random_ned" and (W, H, spp, args.n) == (W0, H0, spp0, 487)
-        metric = BASELINE_METRIC if args.workload == "random_ned" else f"Mray/s + Msample/s, {label} {W0}×{H0}×{spp0}spp"
+        # the metric names the frame this run rendered (the BASELINE metric only for config 2 exactly)
+        metric = BASELINE_METRIC if is_baseline_cfg else f"Mray/s + Msample/s, {label} {W}×{H}×{spp}spp"
         out = {
             "metric": metric,
             "value": round(segs_all / elapsed / 1e6, 2),

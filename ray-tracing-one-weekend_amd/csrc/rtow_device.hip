@@ -974,6 +974,99 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
     return ~(uint32_t)rkey;
 }
 
+// trace_simple over the 4-wide tree (DWide, MODE 7): an INNER step slab-tests
+// its four child boxes, visits the nearest hit child next and pushes the
+// others far to near; a LEAF step tests its spheres in a loop (the same
+// sphere arithmetic and 64-bit record key as trace_simple's sphere slots, so
+// the record is the same whatever the tree).  Every lane of a wave at an
+// inner node runs the box work, every lane at a leaf the sphere loop: a step
+// runs the sphere path only for lanes at leaves (trace_simple: for any lane
+// whose node has a sphere slot).
+// Node references are 16 bits (WIDE_LEAF | node index; WIDE_NONE: none) and
+// the stack holds them as 16-bit entries: the lane's LDS column of STACK words
+// holds 2 STACK entries (an inner step can push three).
+constexpr uint32_t WIDE_LEAF = 0x8000u, WIDE_NONE = 0xFFFFu;
+template <int STACK, int BS>
+__device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* nodes, uint32_t root, const Ray& r,
+                                               float tmin, float& bt, uint32_t* stk32) {
+    const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
+    const float a = dot(r.d, r.d);
+    const float ra = 1.0f / a;
+    const float time = r.time;
+    const uint32_t NONE = WIDE_NONE;
+    // the lane's column: stk32 = stack base + lane; 16-bit entry e at [e * BS]
+    uint16_t* const stk = reinterpret_cast<uint16_t*>(stk32 - (threadIdx.x)) + threadIdx.x;
+    unsigned long long rkey = (unsigned long long)__float_as_uint(bt) << 32 | (uint32_t)~mkref(DK_NONE, 0);
+    // (clamped: an empty child slot's box has every plane at +inf, which no
+    // ray reaches within a finite bound -- see buildWide)
+    float btc = fminf(cull_bound(bt) + q.werr, FLT_MAX);
+    stk[0] = (uint16_t)NONE;  // sentinel (trace_simple)
+    int sp = 1;
+    uint32_t cur = root;
+    while (true) {
+        const float4* np = reinterpret_cast<const float4*>(nodes + (cur & 0x7FFFu));
+        const uint4 refs = reinterpret_cast<const uint4*>(np)[7];
+        uint32_t nxt = NONE;
+        if (!(cur & WIDE_LEAF)) {
+            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
+            float d0, d1, d2, d3;
+            const float INF = __builtin_inff();
+            d0 = slab_f(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, q, tmin, btc, d0) ? d0 : INF;
+            d1 = slab_f(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, q, tmin, btc, d1) ? d1 : INF;
+            d2 = slab_f(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, q, tmin, btc, d2) ? d2 : INF;
+            d3 = slab_f(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, q, tmin, btc, d3) ? d3 : INF;
+            uint32_t r0 = refs.x, r1 = refs.y, r2 = refs.z, r3 = refs.w;
+            // sort (d, ref) ascending: comparators (0,1) (2,3) (0,2) (1,3) (1,2)
+            auto cs = [](float& da, uint32_t& ra_, float& db, uint32_t& rb) {
+                const bool s = db < da;
+                const float t = da;
+                const uint32_t u = ra_;
+                da = s ? db : da;
+                ra_ = s ? rb : ra_;
+                db = s ? t : db;
+                rb = s ? u : rb;
+            };
+            cs(d0, r0, d1, r1);
+            cs(d2, r2, d3, r3);
+            cs(d0, r0, d2, r2);
+            cs(d1, r1, d3, r3);
+            cs(d1, r1, d2, r2);
+            // far to near onto the stack, the nearest next (an empty slot's
+            // box is empty: never hit)
+            if (d3 < INF) stk[sp++ * BS] = (uint16_t)r3;
+            if (d2 < INF) stk[sp++ * BS] = (uint16_t)r2;
+            if (d1 < INF) stk[sp++ * BS] = (uint16_t)r1;
+            nxt = d0 < INF ? r0 : NONE;
+        } else {
+            const float4 s0 = np[0], s1 = np[1], s2 = np[2], s3 = np[3], m0 = np[4], m1 = np[5], m2 = np[6];
+            const uint32_t sr[4] = {refs.x, refs.y, refs.z, refs.w};
+            const float4 sc[4] = {s0, s1, s2, s3};
+            const float dcv[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if ((sr[k] >> KIND_SHIFT) == DK_NONE) break;
+                const F3 c = add(f3(sc[k].x, sc[k].y, sc[k].z), scl(time, f3(dcv[3 * k], dcv[3 * k + 1], dcv[3 * k + 2])));
+                float t;
+                if (sph_root(c, sc[k].w, r, a, ra, tmin, t)) {
+                    const unsigned long long kk = (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)~sr[k];
+                    if (kk < rkey) {
+                        rkey = kk;
+                        btc = cull_bound(t) + q.werr;
+                    }
+                }
+            }
+        }
+        if (nxt == NONE) {  // pop (entry 0: the sentinel)
+            nxt = stk[(sp - 1) * BS];
+            sp = max(sp - 1, 1);
+        }
+        if (nxt == NONE) break;
+        cur = nxt;
+    }
+    bt = __uint_as_float((uint32_t)(rkey >> 32));
+    return ~(uint32_t)rkey;
+}
+
 // A BvhNode of unit-time spheres inside a general scene (TOP_SPHERES: a
 // top-level item that is a chain of instances over one), traversed in a loop
 // of its own: dnode_step's node step on the DNode twins (spheres inline, the
@@ -1398,8 +1491,20 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             box6_scan(S, T.a, r, inv, tmin, bt, bp);
         } else if (kind == TOP_RECTS) {
             for (uint32_t k = 0; k < T.b; k++) {
+                // the rectangle is the same for the whole wave (a scalar load):
+                // its axes pick rect_t_ax's compile-time variant by a uniform
+                // branch instead of rect_t's per-component selects
+                const DRect q = cld(S.rect + T.a + k);
+                const uint32_t ax = q.axis & 3u;
                 float t;
-                if (rect_t(cld(S.rect + T.a + k), r, inv, tmin, bt, t)) take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k));
+                bool h;
+                if (ax == 0)
+                    h = rect_t_ax<2, 0, 1>(q.a0, q.a1, q.b0, q.b1, q.k, r, inv, tmin, bt, t);
+                else if (ax == 1)
+                    h = rect_t_ax<1, 0, 2>(q.a0, q.a1, q.b0, q.b1, q.k, r, inv, tmin, bt, t);
+                else
+                    h = rect_t_ax<0, 1, 2>(q.a0, q.a1, q.b0, q.b1, q.k, r, inv, tmin, bt, t);
+                if (h) take_hit(S, t, bt, bp, mkref(DK_RECT, T.a + k));
             }
         } else if (TOPMED && kind == TOP_MEDIUM) {
             // ConstantMedium::hit (constantMedium.h:26-74) with the closest hit
@@ -2207,9 +2312,9 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                                                        unsigned long long* fx, unsigned long long* counters) {
     Prof prof{};
     unsigned long long t_mark = PROF ? __builtin_amdgcn_s_memtime() : 0;
-    constexpr bool SIMPLE = MODE == 0;
+    constexpr bool SIMPLE = MODE == 0 || MODE == 7;  // 7: the simple scene over its 4-wide tree
     static_assert(STACK * 64 >= 640, "wave_turbulence scratch lives in the wave's stack columns");
-    static_assert(MODE == 0 || BS == BLOCK, "the general traversal strides its LDS stack by BLOCK");
+    static_assert(SIMPLE || BS == BLOCK, "the general traversal strides its LDS stack by BLOCK");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* s_ranvec = reinterpret_cast<float4*>(smem);
     uint32_t* s_perm = reinterpret_cast<uint32_t*>(smem + 4096);
@@ -2219,11 +2324,14 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
         s_perm[i] = S.perm[i];
     }
     const DNode* nodes = S.node;
+    const DWide* wnodes = S.wide;
     if constexpr (SIMPLE && LDSN) {
         float4* s_node = reinterpret_cast<float4*>(smem + 5120 + (size_t)STACK * BS * 4);
-        const float4* g = reinterpret_cast<const float4*>(S.node);
-        for (uint32_t i = threadIdx.x; i < S.n_node * 4u; i += BS) s_node[i] = g[i];
+        const float4* g = reinterpret_cast<const float4*>(MODE == 7 ? (const void*)S.wide : (const void*)S.node);
+        const uint32_t n4 = MODE == 7 ? S.n_wide * 8u : S.n_node * 4u;
+        for (uint32_t i = threadIdx.x; i < n4; i += BS) s_node[i] = g[i];
         nodes = reinterpret_cast<const DNode*>(s_node);
+        wnodes = reinterpret_cast<const DWide*>(s_node);
     }
     __syncthreads();
     const Tables T{s_ranvec, s_perm};
@@ -2313,7 +2421,11 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             }
             const Ray lray = root_ray(S, ray);
             float bt = FLT_MAX;
-            const uint32_t prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
+            uint32_t prim;
+            if constexpr (MODE == 7)
+                prim = trace_wide<STACK, BS>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
+            else
+                prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
             hit = (prim >> KIND_SHIFT) != DK_NONE;
             if constexpr (PROF) {
                 const unsigned long long t_now = __builtin_amdgcn_s_memtime();
@@ -2581,7 +2693,8 @@ __global__ void assemble_lin_kernel(uint32_t W, uint32_t H, uint32_t world, uint
 #define RTOW_KLIST_G(X, M)                                                                         \
     RTOW_K_COMMON(X, M, 16) RTOW_K_PROF(X, M, 16) RTOW_K_COMMON(X, M, 20) RTOW_K_PROF(X, M, 20)   \
     RTOW_K_COMMON(X, M, 32) RTOW_K_PROF(X, M, 32) RTOW_K_DEEP(X, M)
-#define RTOW_K_HOT(X) X(0, 16, 4, false, 512, true, false)
+#define RTOW_K_HOT(X) X(0, 16, 4, false, 512, true, false) X(7, 16, 4, false, 512, true, false) \
+    X(7, 32, 4, false, 512, true, false)
 #define RTOW_KLIST_6(X) RTOW_K_COMMON(X, 6, 16) RTOW_K_PROF(X, 6, 16)
 #if defined(RTOW_TU_SIMPLE)
 #define RTOW_KX(M, S, W, P, B, L, D) template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
@@ -2674,6 +2787,9 @@ struct HostLayout {
     std::vector<uint32_t> xrefs;
     uint32_t xroot = 0;
     uint32_t xdepth = 0;  // rawDepth of the raw graph (general and exact worlds): xhit's frames per thread
+    // simple scenes, RTOW_WIDE: the 4-wide tree (MODE 7)
+    std::vector<DWide> wide;
+    uint32_t wide_root = 0, wide_need = 0;
 };
 
 // The deepest hit() recursion the reference runs over the raw graph (xhit's
@@ -3423,6 +3539,218 @@ bool rebuildSah(HostLayout& L) {
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// The 4-wide tree of a simple scene (MODE 7, RTOW_WIDE=k): a binary SAH tree
+// whose leaves are clusters of at most k spheres, collapsed into nodes of up
+// to four children (the inner child with the largest surface area is opened
+// until four children or only leaves remain).  Sphere slots of the binary
+// tree (trace_simple) put a sphere test and a box test into the same step;
+// here a node is all boxes or all spheres (DWide).  The closest hit does not
+// depend on the tree (the record key settles ties by sphere index).
+struct WBin {
+    float mn[3], mx[3];
+    int l = -1, r = -1;  // children (binary); -1: a leaf cluster P[lo, hi)
+    uint32_t lo = 0, hi = 0;
+};
+
+int wideBin(std::vector<SahPrim>& P, size_t lo, size_t hi, std::vector<WBin>& B, uint32_t leafmax) {
+    const int idx = (int)B.size();
+    B.push_back(WBin{});
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (size_t i = lo; i < hi; i++) sahUnion(mn, mx, P[i].mn, P[i].mx);
+    for (int a = 0; a < 3; a++) {
+        B[idx].mn[a] = mn[a];
+        B[idx].mx[a] = mx[a];
+    }
+    const size_t n = hi - lo;
+    if (n <= leafmax) {
+        B[idx].lo = (uint32_t)lo;
+        B[idx].hi = (uint32_t)hi;
+        return idx;
+    }
+    int best_axis = 0;
+    size_t best_i = lo + n / 2;
+    double best_cost = DBL_MAX;
+    std::vector<float> right_area(n + 1);
+    for (int axis = 0; axis < 3; axis++) {
+        std::sort(P.begin() + lo, P.begin() + hi, [axis](const SahPrim& x, const SahPrim& y) {
+            return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.ref < y.ref);
+        });
+        float rmn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, rmx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = n; k-- > 1;) {
+            sahUnion(rmn, rmx, P[lo + k].mn, P[lo + k].mx);
+            right_area[k] = sahArea(rmn, rmx);
+        }
+        float lmn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lmx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = 1; k < n; k++) {
+            sahUnion(lmn, lmx, P[lo + k - 1].mn, P[lo + k - 1].mx);
+            const double cost = (double)sahArea(lmn, lmx) * (double)k + (double)right_area[k] * (double)(n - k);
+            if (cost < best_cost) {
+                best_cost = cost;
+                best_axis = axis;
+                best_i = lo + k;
+            }
+        }
+    }
+    std::sort(P.begin() + lo, P.begin() + hi, [best_axis](const SahPrim& x, const SahPrim& y) {
+        return x.c[best_axis] < y.c[best_axis] || (x.c[best_axis] == y.c[best_axis] && x.ref < y.ref);
+    });
+    const int l = wideBin(P, lo, best_i, B, leafmax);
+    const int r = wideBin(P, best_i, hi, B, leafmax);
+    B[idx].l = l;
+    B[idx].r = r;
+    return idx;
+}
+
+// emit binary node b as a DWide node (and its subtree); `need`: the stack
+// entries its traversal can hold (an inner step pushes up to children - 1)
+uint32_t wideEmit(const HostLayout& L, const std::vector<SahPrim>& P, const std::vector<WBin>& B, int b,
+                  std::vector<DWide>& out, uint32_t& need) {
+    const uint32_t idx = (uint32_t)out.size();
+    out.push_back(DWide{});
+    if (B[b].l < 0) {  // a leaf cluster
+        DWide w{};
+        for (int k = 0; k < 4; k++) w.ref[k] = mkref(DK_NONE, 0);
+        for (uint32_t i = B[b].lo, k = 0; i < B[b].hi; i++, k++) {
+            const DSphere& sp = L.sph[P[i].ref & INDEX_MASK];
+            w.f[4 * k] = sp.c0[0];
+            w.f[4 * k + 1] = sp.c0[1];
+            w.f[4 * k + 2] = sp.c0[2];
+            w.f[4 * k + 3] = sp.r * sp.r;
+            for (int a = 0; a < 3; a++) w.f[16 + 3 * k + a] = sp.dc[a];
+            w.ref[k] = P[i].ref;
+        }
+        out[idx] = w;
+        need = 0;
+        return WIDE_LEAF | idx;
+    }
+    std::vector<int> ch = {B[b].l, B[b].r};
+    while (ch.size() < 4) {
+        int best = -1;
+        float ba = -1.0f;
+        for (size_t k = 0; k < ch.size(); k++) {
+            if (B[ch[k]].l < 0) continue;
+            const float a = sahArea(B[ch[k]].mn, B[ch[k]].mx);
+            if (a > ba) {
+                ba = a;
+                best = (int)k;
+            }
+        }
+        if (best < 0) break;
+        const int e = ch[best];
+        ch.erase(ch.begin() + best);
+        ch.push_back(B[e].l);
+        ch.push_back(B[e].r);
+    }
+    DWide w{};
+    for (int q = 0; q < 24; q++) w.f[q] = INFINITY;  // empty slots: every plane at +inf (trace_wide)
+    uint32_t deepest = 0;
+    for (size_t k = 0; k < 4; k++) w.ref[k] = WIDE_NONE;
+    for (size_t k = 0; k < ch.size(); k++) {
+        uint32_t nk = 0;
+        w.ref[k] = wideEmit(L, P, B, ch[k], out, nk);
+        deepest = std::max(deepest, nk);
+        for (int a = 0; a < 3; a++) {
+            w.f[8 * a + k] = B[ch[k]].mn[a];
+            w.f[8 * a + 4 + k] = B[ch[k]].mx[a];
+        }
+    }
+    out[idx] = w;
+    need = (uint32_t)ch.size() - 1 + deepest;
+    return idx;
+}
+
+// L.wide / wide_root / wide_need from the simple scene's spheres (after the
+// SAH rebuild: the same leaves, numbered in the reference tree's order)
+void buildWide(HostLayout& L, uint32_t leafmax, uint32_t ref_root) {
+    std::vector<uint32_t> leaves;
+    inorderLeaves(L, ref_root, leaves);
+    if (leaves.size() < 2) return;
+    std::vector<SahPrim> P(leaves.size());
+    for (size_t i = 0; i < leaves.size(); i++) {
+        const DSphere& sp = L.sph[leaves[i] & INDEX_MASK];
+        SahPrim& q = P[i];
+        for (int a = 0; a < 3; a++) {
+            const float c1 = sp.c0[a] + sp.dc[a];
+            q.mn[a] = std::min(sp.c0[a], c1) - sp.r;
+            q.mx[a] = std::max(sp.c0[a], c1) + sp.r;
+            q.c[a] = 0.5f * (q.mn[a] + q.mx[a]);
+        }
+        q.ref = leaves[i];
+    }
+    std::vector<WBin> B;
+    const int root = wideBin(P, 0, P.size(), B, std::max(1u, std::min(4u, leafmax)));
+    L.wide.clear();
+    L.wide_root = wideEmit(L, P, B, root, L.wide, L.wide_need);
+    if (L.wide.size() >= 0x7FFFu) {  // (16-bit node references)
+        L.wide.clear();
+        return;
+    }
+    // the boxes to the world frame, as shiftBoxes does for the DNodes
+    float t[3] = {L.tshift[0], L.tshift[1], L.tshift[2]};
+    if (t[0] != 0.0f || t[1] != 0.0f || t[2] != 0.0f) {
+        auto down = [](double v) {
+            float f = (float)v;
+            return (double)f > v ? std::nextafter(f, -INFINITY) : f;
+        };
+        auto up = [](double v) {
+            float f = (float)v;
+            return (double)f < v ? std::nextafter(f, INFINITY) : f;
+        };
+        for (DWide& w : L.wide) {
+            if ((w.ref[0] >> KIND_SHIFT) == DK_SPHERE) continue;  // a leaf (slot 0 always holds a sphere)
+            for (int a = 0; a < 3; a++)
+                for (int k = 0; k < 4; k++) {
+                    if (w.ref[k] == WIDE_NONE) continue;
+                    w.f[8 * a + k] = down((double)w.f[8 * a + k] + t[a]);
+                    w.f[8 * a + 4 + k] = up((double)w.f[8 * a + 4 + k] + t[a]);
+                }
+        }
+    }
+}
+
+// What trace_wide relies on: every node reachable from the root is an inner
+// node whose non-empty slots (a prefix) reference existing nodes, or a leaf
+// whose non-empty slots (a prefix, at least one) are spheres; each node is
+// reached once (a tree: the traversal cannot cycle); and no path pushes more
+// than wide_need entries.
+bool checkWide(const HostLayout& L) {
+    const size_t n = L.wide.size();
+    std::vector<char> seen(n, 0);
+    std::function<bool(uint32_t, int, uint32_t&)> walk = [&](uint32_t ref, int depth, uint32_t& need) -> bool {
+        const uint32_t i = ref & 0x7FFFu;
+        if (ref == WIDE_NONE || i >= n || depth > 64 || seen[i]) return false;
+        seen[i] = 1;
+        const DWide& w = L.wide[i];
+        need = 0;
+        if (ref & WIDE_LEAF) {
+            int k = 0;
+            while (k < 4 && (w.ref[k] >> KIND_SHIFT) == DK_SPHERE && (w.ref[k] & INDEX_MASK) < L.sph.size()) k++;
+            for (int j = k; j < 4; j++)
+                if (w.ref[j] != mkref(DK_NONE, 0)) return false;
+            return k > 0;
+        }
+        int nch = 0;
+        uint32_t deepest = 0;
+        for (int k = 0; k < 4; k++) {
+            if (w.ref[k] == WIDE_NONE) {
+                for (int a = 0; a < 6; a++)
+                    if (!(w.f[4 * a + k] == INFINITY)) return false;  // an empty slot: never hit
+                continue;
+            }
+            if (nch != k) return false;  // children first
+            nch++;
+            uint32_t nk = 0;
+            if (!walk(w.ref[k], depth + 1, nk)) return false;
+            deepest = std::max(deepest, nk);
+        }
+        need = (uint32_t)std::max(nch - 1, 0) + deepest;
+        return nch >= 2;
+    };
+    uint32_t need = 0;
+    return walk(L.wide_root, 0, need) && need <= L.wide_need;
+}
+
 // A simple scene whose root chain is translations only: its DNode boxes move
 // to the world frame (rounded outward), where the rays' origins lie near them
 // and the one-FMA slab planes stay tight (SlabRay); the kernel shifts each
@@ -4088,7 +4416,7 @@ bool textureNeedsUv(const rtow_scene& s, uint32_t ti, int guard = 0) {
     return false;
 }
 
-int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
+int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH, uint32_t wide = 0) {
     if (s.root >= s.n_hitables || !s.hitables || !s.materials || !s.textures || !s.perlin)
         return set_error(RTOW_E_INVALID, "incomplete scene");
     for (uint32_t i = 0; i < s.n_hitables; i++) {
@@ -4147,9 +4475,14 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH) {
                     }
                 }
             }
-            if (tree == RTOW_TREE_SAH && (L.bvh_root >> KIND_SHIFT) == DK_BVH) rebuildSah(L);
+            const uint32_t ref_root = L.bvh_root;
+            const bool sah = tree == RTOW_TREE_SAH && (L.bvh_root >> KIND_SHIFT) == DK_BVH && rebuildSah(L);
             shiftBoxes(L);
             if (!checkSimpleNodes(L)) return set_error(RTOW_E_INVALID, "internal: simple-scene tree check failed");
+            if (sah && wide) {
+                buildWide(L, wide, ref_root);
+                if (!L.wide.empty() && !checkWide(L)) return set_error(RTOW_E_INVALID, "internal: 4-wide tree check failed");
+            }
         }
     }
     for (uint32_t i = 0; i < s.n_materials; i++) {
@@ -4319,6 +4652,7 @@ struct rtow_context {
     int lds_nodes = 1;  // simple-scene BVH staged in LDS when it fits (RTOW_LDS_NODES=0 disables; +11%, tools/ab.py)
     uint32_t auto_spc = 0;  // samples per work item under automatic chunking (RTOW_AUTO_SPC; 0: from the grid, makeParams)
     int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
+    uint32_t wide = 0;  // RTOW_WIDE=k: simple scenes over a 4-wide tree with leaves of <= k spheres (MODE 7)
     // rtow_debug_trace_sample (a render with the segment-recording kernel)
     float* dbg_out = nullptr;
     uint32_t dbg_col = 0, dbg_row = 0, dbg_sample = 0, dbg_max = 0;
@@ -4366,7 +4700,8 @@ int ensure(void** p, size_t* have, size_t need) {
 
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
-    const size_t lds = lds_bytes(STACK, BS, c->scene.n_node, LDSN, MODE != 0);
+    const size_t lds = lds_bytes(STACK, BS, MODE == 7 ? 2u * c->scene.n_wide : c->scene.n_node, LDSN,
+                                 MODE != 0 && MODE != 7);
     // the occupancy query is host work between the launch events: once per
     // (kernel, LDS size) per process
     static std::mutex mu;
@@ -4391,7 +4726,7 @@ int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
     uint32_t maxUseful = (P.n_items + BS - 1) / BS;
     if (grid > maxUseful) grid = std::max(1u, maxUseful);
     DevParams Pk = P;
-    if constexpr (MODE != 0) {  // xhit's call frames, one column per grid thread, as deep as the world's recursion
+    if constexpr (MODE != 0 && MODE != 7) {  // xhit's call frames, one column per grid thread, as deep as the world's recursion
         Pk.xstride = grid * (uint32_t)BS;
         const int rc = ensure((void**)&c->d_xframes, &c->xframes_bytes,
                               (size_t)Pk.xstride * c->scene.xdepth * sizeof(XFrame));
@@ -4439,9 +4774,21 @@ int launchStack(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
     return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
 }
 
+// MODE 7: the simple scene over its 4-wide tree (RTOW_WIDE), 512-thread
+// blocks with the tree in LDS, the only variants built (hot kernel TU)
+int launchWide(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
+    const uint32_t need = c->scene.wide_need + 1;  // (+ the sentinel entry; 16-bit entries, two per stack word)
+    if (need <= 32 && lds_bytes(16, 512, 2 * c->scene.n_wide, true) <= 80 * 1024)
+        return launchTrace<7, 16, 4, false, 512, true>(c, cam, P, bpc, st);
+    if (need <= 64 && lds_bytes(32, 512, 2 * c->scene.n_wide, true) <= 80 * 1024)
+        return launchTrace<7, 32, 4, false, 512, true>(c, cam, P, bpc, st);
+    return launchStack<0>(c, cam, P, bpc, st);  // too large for LDS: the binary tree (same frame)
+}
+
 int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const DevScene& d = c->scene;
     if (d.exact) return launchWaves<6, 16>(c, cam, P, bpc, st);
+    if (d.simple && d.unit_time && d.n_wide && !c->dbg_out && !c->profile) return launchWide(c, cam, P, bpc, st);
     if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
     if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
     if (!d.media_any && !d.media_nested) return launchStack<5>(c, cam, P, bpc, st);
@@ -4685,6 +5032,7 @@ int rtow_context_create(int device, rtow_context** out) {
     if (const char* ln = std::getenv("RTOW_LDS_NODES")) c->lds_nodes = std::atoi(ln);
     if (const char* sc = std::getenv("RTOW_AUTO_SPC")) c->auto_spc = std::max(1, std::atoi(sc));
     if (const char* tr = std::getenv("RTOW_BVH")) c->tree = std::string(tr) == "ref" ? RTOW_TREE_REFERENCE : RTOW_TREE_SAH;
+    if (const char* wd = std::getenv("RTOW_WIDE")) c->wide = (uint32_t)std::max(0, std::atoi(wd));
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
@@ -4717,6 +5065,19 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
     int rc = buildLayout(*s, L);
     if (rc) return rc;
     if (L.stack_need > 64) return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
+    if (std::getenv("RTOW_LAYOUT_INFO") && std::getenv("RTOW_WIDE")) {
+        HostLayout W;
+        if (buildLayout(*s, W, RTOW_TREE_SAH, (uint32_t)std::atoi(std::getenv("RTOW_WIDE"))) == RTOW_OK) {
+            size_t leaves = 0, spheres = 0;
+            for (const DWide& w : W.wide)
+                if ((w.ref[0] >> KIND_SHIFT) == DK_SPHERE) {  // (a leaf)
+                    leaves++;
+                    for (int k = 0; k < 4; k++) spheres += (w.ref[k] >> KIND_SHIFT) == DK_SPHERE;
+                }
+            std::fprintf(stderr, "rtow-layout: wide nodes %zu (leaves %zu holding %zu spheres) root %08x need %u\n",
+                         W.wide.size(), leaves, spheres, W.wide_root, W.wide_need);
+        }
+    }
     if (std::getenv("RTOW_LAYOUT_INFO"))
         std::fprintf(stderr,
                      "rtow-layout: simple %d gnode %d nodes %zu bvh %zu spheres %zu rects %zu lists %zu insts %zu media %zu "
@@ -4724,6 +5085,10 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
                      (int)L.simple, (int)L.gnode, L.node.size(), L.bvh.size(), L.sph.size(), L.rect.size(), L.list.size(),
                      L.inst.size(), L.med.size(), L.top.size(), L.stack_need, L.chain_need, (int)L.media_nested,
                      (int)L.media_any);
+    if (std::getenv("RTOW_LAYOUT_INFO"))
+        for (size_t j = 0; j < L.top.size(); j++)
+            std::fprintf(stderr, "rtow-layout: top[%zu] kind %u flags %03x a %08x b %u chain %u\n", j,
+                         L.top[j].kind & TOP_KIND_MASK, L.top[j].kind >> 8, L.top[j].a, L.top[j].b, L.top[j].chain);
     if (stack_need) *stack_need = L.stack_need;
     if (chain_need) *chain_need = L.chain_need;
     return RTOW_OK;
@@ -4756,7 +5121,7 @@ int rtow_context_set_tree(rtow_context* c, int tree) {
 int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     if (!c || !s) return set_error(RTOW_E_INVALID, "NULL argument");
     HostLayout L;
-    int rc = buildLayout(*s, L, c->tree);
+    int rc = buildLayout(*s, L, c->tree, c->wide);
     if (rc) return rc;
     std::vector<uint8_t> blob;
     size_t o_bvh = pushBlob(blob, L.bvh), o_node = pushBlob(blob, L.node), o_sph = pushBlob(blob, L.sph);
@@ -4796,6 +5161,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     if (L.xh.empty()) L.xh.push_back(XHit{});
     if (L.xrefs.empty()) L.xrefs.push_back(0u);
     size_t o_xh = pushBlob(blob, L.xh), o_xrefs = pushBlob(blob, L.xrefs);
+    const uint32_t n_wide = (uint32_t)L.wide.size();
+    if (L.wide.empty()) L.wide.push_back(DWide{});
+    size_t o_wide = pushBlob(blob, L.wide);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -4851,6 +5219,10 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.xroot = L.xroot;
     d.exact = L.exact ? 1u : 0u;
     d.xdepth = std::max(1u, L.xdepth);
+    d.wide = (const DWide*)(b + o_wide);
+    d.n_wide = n_wide;
+    d.wide_root = L.wide_root;
+    d.wide_need = L.wide_need;
     c->has_scene = true;
     // progressive sums belong to the scene they were rendered from: a new
     // scene restarts them (rtow_render_progressive)

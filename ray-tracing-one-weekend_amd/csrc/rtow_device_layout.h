@@ -75,6 +75,20 @@ struct alignas(16) DNode {
     uint32_t ref_b;
 };
 
+// The 4-wide tree of a simple scene (MODE 7, RTOW_WIDE): every node is either
+// INNER -- up to four child boxes, x/y/z planes as SoA (lo_x[4] hi_x[4]
+// lo_y[4] hi_y[4] lo_z[4] hi_z[4] in f[0..23]), children referenced by ref[k]
+// (DK_BVH: an inner node, DK_LIST: a leaf node, DK_NONE: empty, its box empty)
+// -- or LEAF -- up to four spheres, k-th at f[4k..4k+3] = center0 xyz, r*r and
+// f[16+3k..18+3k] = center1 - center0, ref[k] = DK_SPHERE | sphere index
+// (DK_NONE after the last).  A step of the traversal runs one kind of work
+// for every lane at that kind of node: four slab tests, or a loop of sphere
+// tests.
+struct alignas(16) DWide {  // 128 B
+    float f[28];
+    uint32_t ref[4];
+};
+
 // Sphere (sphere.h:7-18) and MovingSphere (sphere.h:76-91) share one leaf:
 // a static sphere is stored with center1 = center0, time0 = 0, time1 = 1, and
 // center(time) = c0 + ((time-0)/(1-0)) * (c0-c0) = c0 exactly, so one test
@@ -276,6 +290,11 @@ struct DevScene {
     uint32_t xroot;
     uint32_t exact;
     uint32_t xdepth;  // the deepest hit() recursion of the raw graph (rawDepth, <= XDEPTH): xhit's frames per thread
+    // simple scenes with a 4-wide tree (MODE 7): nodes, count, root ref and stack need
+    const DWide* wide;
+    uint32_t n_wide;
+    uint32_t wide_root;
+    uint32_t wide_need;
 };
 
 // One reference Hitable, as rtow_hitable (include/rtow.h) lays it out.

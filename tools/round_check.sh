@@ -22,7 +22,7 @@ if [[ $STEPS == *general* ]]; then
     bash tools/profile_bench.sh ${TAG}_$w --workload $w --cpu-pixels 2000 > gpurun_out/profile_${TAG}_$w.log 2>&1 || exit $?
   done
   # config 5 at its full 4096x4096 frame, 256 spp per launch (VALU per ray does not depend on spp)
-  bash tools/profile_bench.sh ${TAG}_final_ned --workload final_ned --spp 256 --cpu-pixels 300 --cpu-spp 256 \
+  bash tools/profile_bench.sh ${TAG}_final_ned --workload final_ned --spp 256 --cpu-pixels 8000 --cpu-spp 512 \
       > gpurun_out/profile_${TAG}_final_ned.log 2>&1 || exit $?
 fi
 if [[ $STEPS == *configs* ]]; then
