@@ -433,16 +433,21 @@ __device__ __forceinline__ float div_by_any(float x, float a, float ra) {
 
 // The sphere tests' sqrt(disc), disc > 0: v_sqrt_f32 (within 1 ulp) and the
 // two one-ulp FMA residual corrections of sqrtf's own expansion, without its
-// rescaling of inputs below 2^-96 and its selects for 0 / inf / NaN (7 VALU
-// of a sphere test's 17).  tools/sqrt_check.hip compares it with sqrtf on
-// every positive float: equal for every x >= 2^-96 and +inf, off for smaller
-// ones (v_sqrt_f32's error there exceeds one ulp; the result stays below
-// 2^-48).  A root (-b -+ sq) / a can only notice that when |b| < 2^-22 as
-// well -- a ray leaving a point of the sphere's surface within ~2^-22 of a
-// tangent with disc = b*b - a*c below 2^-96 -- which no frame of the test
-// suite or the configs meets (segment counts equal the oracle's).
-// RTOW_SQRT_POS: 1 (default) this; 2 with sqrtf's rescaling (equal to sqrtf
-// for every positive float: -1.8 % on config 2, tools/ab.py); 0 sqrtf.
+// selects for 0 / inf / NaN.  !FAST keeps sqrtf's rescaling of inputs below
+// 2^-96 and equals sqrtf for every positive float (tools/sqrt_check.hip
+// checks all of them on the GPU).  FAST drops the rescaling (7 VALU of a
+// sphere test's 17; config 2 +1.8 %): equal for every x >= 2^-96 and +inf,
+// off for smaller ones (v_sqrt_f32's error there exceeds one ulp; the result
+// stays below 2^-48).  Where that can reach a frame: a root (-b -+ sq) / a is
+// accepted only above tmin = 0.001; disc in (0, 2^-96) forces b*b < 2^-70
+// (else b*b - a*c is 0 or at least 2^-96: Sterbenz), so |-b -+ sq| < 2^-34.9
+// and the root is below 2^-34.9 / a -- under tmin unless a = dot(d, d) <
+// 2^-24.  The simple-scene traversal therefore runs FAST only for rays with
+// dot(d, d) >= 2^-24 (every camera ray, all but a vanishing fraction of
+// Lambertian bounces, (p + n + r) - p with r within 2^-12 of -n) and the exact
+// variant for the rest; the general kernels use the exact variant
+// (tests/test_gpu_sqrt.py constructs such a ray).  RTOW_SQRT_POS=0: sqrtf;
+// 2: the exact variant everywhere.
 #ifndef RTOW_SQRT_POS
 #define RTOW_SQRT_POS 1
 #endif
@@ -456,23 +461,20 @@ __device__ __forceinline__ float div_by_any(float x, float a, float ra) {
 #define RTOW_ROOT_SEL 0
 #endif
 #endif
+template <bool FAST>
 __device__ __forceinline__ float sqrt_pos(float x) {
 #if RTOW_SQRT_POS
-#if RTOW_SQRT_POS == 2
-    const bool small = x < 0x1p-96f;
-    x = small ? x * 0x1p32f : x;
-#endif
+    constexpr bool F = FAST && RTOW_SQRT_POS == 1;
+    const bool small = !F && x < 0x1p-96f;
+    if constexpr (!F) x = small ? x * 0x1p32f : x;
     const float s = __builtin_amdgcn_sqrtf(x);
     const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
     const float sup = __uint_as_float(__float_as_uint(s) + 1u);
     const float rdn = fmaf(-sdn, s, x), rup = fmaf(-sup, s, x);
     const float t = rdn <= 0.0f ? sdn : s;
-#if RTOW_SQRT_POS == 2
     const float u = rup > 0.0f ? sup : t;
+    if constexpr (F) return u;
     return small ? u * 0x1p-16f : u;
-#else
-    return rup > 0.0f ? sup : t;
-#endif
 #else
     return sqrtf(x);
 #endif
@@ -487,7 +489,7 @@ __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, 
     const float c = dot(oc, oc) - radius * radius;
     const float disc = b * b - a * c;
     if (disc > 0) {
-        const float sq = sqrt_pos(disc);
+        const float sq = sqrt_pos<false>(disc);
         const float tn = div_by(-b - sq, a, ra);
         if (tn < tmax && tn > tmin) {
             t = tn;
@@ -509,6 +511,7 @@ __device__ __forceinline__ bool sph_quad(F3 center, float radius, const Ray& r, 
 // record so far.  The far root is only evaluated when the near one is <= tmin.
 // rr: radius * radius (a DNode's sphere slot holds it, rounded as the
 // reference's radius*radius is)
+template <bool FAST = false>
 __device__ __forceinline__ bool sph_root(F3 center, float rr, const Ray& r, float a, float ra, float tmin,
                                          float& t) {
     const F3 oc = sub(r.o, center);
@@ -516,7 +519,7 @@ __device__ __forceinline__ bool sph_root(F3 center, float rr, const Ray& r, floa
     const float c = dot(oc, oc) - rr;
     const float disc = b * b - a * c;
     if (disc > 0) {
-        const float sq = sqrt_pos(disc);
+        const float sq = sqrt_pos<FAST>(disc);
         // the near root, or the far one when the near is not above tmin; the
         // far root is never below the near one (-b + sq >= -b - sq, a > 0), so
         // a near root >= FLT_MAX leaves none (Sphere::hit's two tests)
@@ -853,7 +856,7 @@ __device__ __forceinline__ uint32_t dnode_step(const DevScene& S, uint32_t idx, 
 // The stack keeps its top entry in a register: a pop hands that entry to the
 // next node fetch at once while the LDS read of the new top is in flight.
 // Returns the winning sphere ref or DK_NONE.
-template <int STACK, int BS, bool PROF>
+template <int STACK, int BS, bool PROF, bool FAST>
 __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode* nodes, uint32_t root, const Ray& r, float tmin,
                                  float& bt, uint32_t* stk, uint32_t& overflow, Prof& prof) {
     // the boxes sit in the world frame (DevScene::tshift, see SlabRay): the
@@ -922,7 +925,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
             // Sphere::hit / MovingSphere::hit with center = c0 + time * (c1 - c0)
             const F3 c = add(f3(b0.x, b0.y, b0.z), scl(time, f3(b1.x, b1.y, b1.z)));
             float t;
-            if (sph_root(c, b0.w, r, a, ra, tmin, t)) {
+            if (sph_root<FAST>(c, b0.w, r, a, ra, tmin, t)) {
                 const unsigned long long k = (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)~refb;
                 if (k < rkey) {
                     rkey = k;
@@ -936,7 +939,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
         if ((refa >> KIND_SHIFT) == DK_SPHERE) {
             const F3 c = add(f3(a0.x, a0.y, a0.z), scl(time, f3(a1.x, a1.y, a1.z)));
             float t;
-            if (sph_root(c, a0.w, r, a, ra, tmin, t)) {
+            if (sph_root<FAST>(c, a0.w, r, a, ra, tmin, t)) {
                 const unsigned long long k = (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)~refa;
                 if (k < rkey) {
                     rkey = k;
@@ -986,7 +989,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
 // the stack holds them as 16-bit entries: the lane's LDS column of STACK words
 // holds 2 STACK entries (an inner step can push three).
 constexpr uint32_t WIDE_LEAF = 0x8000u, WIDE_NONE = 0xFFFFu;
-template <int STACK, int BS>
+template <int STACK, int BS, bool FAST>
 __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* nodes, uint32_t root, const Ray& r,
                                                float tmin, float& bt, uint32_t* stk32) {
     const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
@@ -1047,7 +1050,7 @@ __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* n
                 if ((sr[k] >> KIND_SHIFT) == DK_NONE) break;
                 const F3 c = add(f3(sc[k].x, sc[k].y, sc[k].z), scl(time, f3(dcv[3 * k], dcv[3 * k + 1], dcv[3 * k + 2])));
                 float t;
-                if (sph_root(c, sc[k].w, r, a, ra, tmin, t)) {
+                if (sph_root<FAST>(c, sc[k].w, r, a, ra, tmin, t)) {
                     const unsigned long long kk = (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)~sr[k];
                     if (kk < rkey) {
                         rkey = kk;
@@ -1153,7 +1156,7 @@ __device__ __forceinline__ bool sphere_boundary(const Sph& s, const Ray& r, floa
     const float c = dot(oc, oc) - s.r * s.r;
     const float disc = b * b - a * c;
     if (!(disc > 0)) return false;
-    const float sq = sqrt_pos(disc);
+    const float sq = sqrt_pos<false>(disc);
     const float tn = div_by(-b - sq, a, ra), tf = div_by(-b + sq, a, ra);  // the IEEE quotients (sph_root's)
     const float lo = -FLT_MAX;
     float first;
@@ -2422,10 +2425,20 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             const Ray lray = root_ray(S, ray);
             float bt = FLT_MAX;
             uint32_t prim;
-            if constexpr (MODE == 7)
-                prim = trace_wide<STACK, BS>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
-            else
-                prim = trace_simple<STACK, BS, PROF>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
+            // the fast sphere-test sqrt only for rays where it equals sqrtf's
+            // effect (sqrt_pos: dot(d, d) >= 2^-24), the exact one for the rest
+            const bool fast = dot(lray.d, lray.d) >= 0x1p-24f;
+            if constexpr (MODE == 7) {
+                if (fast)
+                    prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
+                else
+                    prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
+            } else {
+                if (fast)
+                    prim = trace_simple<STACK, BS, PROF, true>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
+                else
+                    prim = trace_simple<STACK, BS, PROF, false>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
+            }
             hit = (prim >> KIND_SHIFT) != DK_NONE;
             if constexpr (PROF) {
                 const unsigned long long t_now = __builtin_amdgcn_s_memtime();
