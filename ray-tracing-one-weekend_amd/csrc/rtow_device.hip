@@ -182,6 +182,7 @@ struct DevParams {
     float* dbg_out;
     struct XFrame* xframes;  // xhit's call frames: DevScene::xdepth x xstride (the grid's threads)
     uint32_t xstride;
+    uint32_t spec;  // MODE 7: postponed leaves (trace_wide_spec) below this many lanes with inner work; 0: off
 };
 
 struct Rec {
@@ -1065,6 +1066,102 @@ __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* n
         }
         if (nxt == NONE) break;
         cur = nxt;
+    }
+    bt = __uint_as_float((uint32_t)(rkey >> 32));
+    return ~(uint32_t)rkey;
+}
+
+// trace_wide with postponed leaves (speculative traversal, RTOW_SPEC = spec):
+// a lane that reaches a leaf parks it (one 16-bit slot) and goes on with the
+// inner nodes on its stack; every iteration the WAVE picks one kind of work --
+// a leaf pass (every lane with a parked leaf tests its spheres) when fewer than
+// `spec` lanes have inner work left and some leaf is parked, an inner pass
+// otherwise -- so no iteration runs both the box and the sphere path.  A lane
+// that meets a second leaf while one is parked waits for the next leaf pass.
+// The record is the same (the key is order-free); parked leaves cull later.
+template <int STACK, int BS, bool FAST>
+__device__ __forceinline__ uint32_t trace_wide_spec(const DevScene& S, const DWide* nodes, uint32_t root, const Ray& r,
+                                                    float tmin, float& bt, uint32_t* stk32, uint32_t spec) {
+    const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
+    const float a = dot(r.d, r.d);
+    const float ra = 1.0f / a;
+    const float time = r.time;
+    const uint32_t NONE = WIDE_NONE;
+    uint16_t* const stk = reinterpret_cast<uint16_t*>(stk32 - (threadIdx.x)) + threadIdx.x;
+    unsigned long long rkey = (unsigned long long)__float_as_uint(bt) << 32 | (uint32_t)~mkref(DK_NONE, 0);
+    float btc = fminf(cull_bound(bt) + q.werr, FLT_MAX);
+    stk[0] = (uint16_t)NONE;
+    int sp = 1;
+    uint32_t cur = root, parked = NONE;
+    while (true) {
+        if (cur != NONE && (cur & WIDE_LEAF) && parked == NONE) {  // park the leaf, go on with the stack
+            parked = cur;
+            cur = stk[(sp - 1) * BS];
+            sp = max(sp - 1, 1);
+        }
+        const bool inner = cur != NONE && !(cur & WIDE_LEAF);
+        const bool leafw = parked != NONE;
+        const unsigned long long mi = __ballot(inner), ml = __ballot(leafw);
+        if ((mi | ml) == 0) break;  // (uniform: every lane of the wave is done)
+        if (ml != 0 && (mi == 0 || (uint32_t)__popcll(mi) < spec)) {
+            if (leafw) {  // the leaf pass
+                const float4* np = reinterpret_cast<const float4*>(nodes + (parked & 0x7FFFu));
+                const uint4 refs = reinterpret_cast<const uint4*>(np)[7];
+                const float4 s0 = np[0], s1 = np[1], s2 = np[2], s3 = np[3], m0 = np[4], m1 = np[5], m2 = np[6];
+                const uint32_t sr[4] = {refs.x, refs.y, refs.z, refs.w};
+                const float4 sc[4] = {s0, s1, s2, s3};
+                const float dcv[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if ((sr[k] >> KIND_SHIFT) == DK_NONE) break;
+                    const F3 c =
+                        add(f3(sc[k].x, sc[k].y, sc[k].z), scl(time, f3(dcv[3 * k], dcv[3 * k + 1], dcv[3 * k + 2])));
+                    float t;
+                    if (sph_root<FAST>(c, sc[k].w, r, a, ra, tmin, t)) {
+                        const unsigned long long kk = (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)~sr[k];
+                        if (kk < rkey) {
+                            rkey = kk;
+                            btc = cull_bound(t) + q.werr;
+                        }
+                    }
+                }
+                parked = NONE;
+            }
+        } else if (inner) {  // the inner pass
+            const float4* np = reinterpret_cast<const float4*>(nodes + (cur & 0x7FFFu));
+            const uint4 refs = reinterpret_cast<const uint4*>(np)[7];
+            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
+            const float INF = __builtin_inff();
+            float d0, d1, d2, d3;
+            d0 = slab_f(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, q, tmin, btc, d0) ? d0 : INF;
+            d1 = slab_f(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, q, tmin, btc, d1) ? d1 : INF;
+            d2 = slab_f(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, q, tmin, btc, d2) ? d2 : INF;
+            d3 = slab_f(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, q, tmin, btc, d3) ? d3 : INF;
+            uint32_t r0 = refs.x, r1 = refs.y, r2 = refs.z, r3 = refs.w;
+            auto cs = [](float& da, uint32_t& ra_, float& db, uint32_t& rb) {
+                const bool s = db < da;
+                const float t = da;
+                const uint32_t u = ra_;
+                da = s ? db : da;
+                ra_ = s ? rb : ra_;
+                db = s ? t : db;
+                rb = s ? u : rb;
+            };
+            cs(d0, r0, d1, r1);
+            cs(d2, r2, d3, r3);
+            cs(d0, r0, d2, r2);
+            cs(d1, r1, d3, r3);
+            cs(d1, r1, d2, r2);
+            if (d3 < INF) stk[sp++ * BS] = (uint16_t)r3;
+            if (d2 < INF) stk[sp++ * BS] = (uint16_t)r2;
+            if (d1 < INF) stk[sp++ * BS] = (uint16_t)r1;
+            if (d0 < INF) {
+                cur = r0;
+            } else {
+                cur = stk[(sp - 1) * BS];
+                sp = max(sp - 1, 1);
+            }
+        }
     }
     bt = __uint_as_float((uint32_t)(rkey >> 32));
     return ~(uint32_t)rkey;
@@ -2429,7 +2526,10 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             // effect (sqrt_pos: dot(d, d) >= 2^-24), the exact one for the rest
             const bool fast = dot(lray.d, lray.d) >= 0x1p-24f;
             if constexpr (MODE == 7) {
-                if (fast)
+                if (P.spec)
+                    prim = fast ? trace_wide_spec<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec)
+                                : trace_wide_spec<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec);
+                else if (fast)
                     prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
                 else
                     prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
@@ -4666,6 +4766,7 @@ struct rtow_context {
     uint32_t auto_spc = 0;  // samples per work item under automatic chunking (RTOW_AUTO_SPC; 0: from the grid, makeParams)
     int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
     uint32_t wide = 0;  // RTOW_WIDE=k: simple scenes over a 4-wide tree with leaves of <= k spheres (MODE 7)
+    uint32_t spec = 0;  // RTOW_SPEC=n: MODE 7 with postponed leaves (trace_wide_spec), leaf pass below n inner lanes
     // rtow_debug_trace_sample (a render with the segment-recording kernel)
     float* dbg_out = nullptr;
     uint32_t dbg_col = 0, dbg_row = 0, dbg_sample = 0, dbg_max = 0;
@@ -4879,6 +4980,7 @@ int planParams(int cus, uint32_t auto_spc, const rtow_params* p, DevParams& P) {
 int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     const int rc = planParams(c->cus, c->auto_spc, p, P);
     if (rc) return rc;
+    P.spec = c->spec;
     P.dbg_out = c->dbg_out;
     P.dbg_col = c->dbg_col;
     P.dbg_row = c->dbg_row;
@@ -5046,6 +5148,7 @@ int rtow_context_create(int device, rtow_context** out) {
     if (const char* sc = std::getenv("RTOW_AUTO_SPC")) c->auto_spc = std::max(1, std::atoi(sc));
     if (const char* tr = std::getenv("RTOW_BVH")) c->tree = std::string(tr) == "ref" ? RTOW_TREE_REFERENCE : RTOW_TREE_SAH;
     if (const char* wd = std::getenv("RTOW_WIDE")) c->wide = (uint32_t)std::max(0, std::atoi(wd));
+    if (const char* sv = std::getenv("RTOW_SPEC")) c->spec = (uint32_t)std::max(0, std::atoi(sv));
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
