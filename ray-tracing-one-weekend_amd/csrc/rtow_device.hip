@@ -992,7 +992,7 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
 constexpr uint32_t WIDE_LEAF = 0x8000u, WIDE_NONE = 0xFFFFu;
 template <int STACK, int BS, bool FAST>
 __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* nodes, uint32_t root, const Ray& r,
-                                               float tmin, float& bt, uint32_t* stk32) {
+                                               float tmin, float& bt, uint32_t* stk32, uint32_t& overflow) {
     const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
     const float a = dot(r.d, r.d);
     const float ra = 1.0f / a;
@@ -1007,7 +1007,12 @@ __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* n
     stk[0] = (uint16_t)NONE;  // sentinel (trace_simple)
     int sp = 1;
     uint32_t cur = root;
+    uint32_t guard = 0;  // (experiment: a step bound that can only fail loudly)
     while (true) {
+        if (++guard > 8192u) {
+            overflow = 1;
+            break;
+        }
         const float4* np = reinterpret_cast<const float4*>(nodes + (cur & 0x7FFFu));
         const uint4 refs = reinterpret_cast<const uint4*>(np)[7];
         uint32_t nxt = NONE;
@@ -1081,7 +1086,8 @@ __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* n
 // The record is the same (the key is order-free); parked leaves cull later.
 template <int STACK, int BS, bool FAST>
 __device__ __forceinline__ uint32_t trace_wide_spec(const DevScene& S, const DWide* nodes, uint32_t root, const Ray& r,
-                                                    float tmin, float& bt, uint32_t* stk32, uint32_t spec) {
+                                                    float tmin, float& bt, uint32_t* stk32, uint32_t spec,
+                                                    uint32_t& overflow) {
     const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
     const float a = dot(r.d, r.d);
     const float ra = 1.0f / a;
@@ -1093,7 +1099,12 @@ __device__ __forceinline__ uint32_t trace_wide_spec(const DevScene& S, const DWi
     stk[0] = (uint16_t)NONE;
     int sp = 1;
     uint32_t cur = root, parked = NONE;
+    uint32_t guard = 0;
     while (true) {
+        if (++guard > 8192u) {  // (uniform: every lane counts the same iterations)
+            overflow = 1;
+            break;
+        }
         if (cur != NONE && (cur & WIDE_LEAF) && parked == NONE) {  // park the leaf, go on with the stack
             parked = cur;
             cur = stk[(sp - 1) * BS];
@@ -2527,12 +2538,14 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
             const bool fast = dot(lray.d, lray.d) >= 0x1p-24f;
             if constexpr (MODE == 7) {
                 if (P.spec)
-                    prim = fast ? trace_wide_spec<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec)
-                                : trace_wide_spec<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec);
+                    prim = fast ? trace_wide_spec<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec,
+                                                                   overflow)
+                                : trace_wide_spec<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec,
+                                                                    overflow);
                 else if (fast)
-                    prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
+                    prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow);
                 else
-                    prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk);
+                    prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow);
             } else {
                 if (fast)
                     prim = trace_simple<STACK, BS, PROF, true>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
@@ -5192,6 +5205,16 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
                 }
             std::fprintf(stderr, "rtow-layout: wide nodes %zu (leaves %zu holding %zu spheres) root %08x need %u\n",
                          W.wide.size(), leaves, spheres, W.wide_root, W.wide_need);
+            if (const char* path = std::getenv("RTOW_WIDE_DUMP")) {  // (tests: the nodes, root, need, tshift, spheres)
+                if (FILE* f = std::fopen(path, "wb")) {
+                    const uint32_t hdr[4] = {(uint32_t)W.wide.size(), W.wide_root, W.wide_need, (uint32_t)W.sph.size()};
+                    std::fwrite(hdr, 4, 4, f);
+                    std::fwrite(W.tshift, 4, 3, f);
+                    std::fwrite(W.wide.data(), sizeof(DWide), W.wide.size(), f);
+                    std::fwrite(W.sph.data(), sizeof(DSphere), W.sph.size(), f);
+                    std::fclose(f);
+                }
+            }
         }
     }
     if (std::getenv("RTOW_LAYOUT_INFO"))
