@@ -183,6 +183,7 @@ struct DevParams {
     struct XFrame* xframes;  // xhit's call frames: DevScene::xdepth x xstride (the grid's threads)
     uint32_t xstride;
     uint32_t spec;  // MODE 7: postponed leaves (trace_wide_spec) below this many lanes with inner work; 0: off
+    uint32_t* wdbg;  // MODE 7 debugging (RTOW_WIDE_DEBUG): the first guard trip's ray and state
 };
 
 struct Rec {
@@ -992,7 +993,8 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
 constexpr uint32_t WIDE_LEAF = 0x8000u, WIDE_NONE = 0xFFFFu;
 template <int STACK, int BS, bool FAST>
 __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* nodes, uint32_t root, const Ray& r,
-                                               float tmin, float& bt, uint32_t* stk32, uint32_t& overflow) {
+                                               float tmin, float& bt, uint32_t* stk32, uint32_t& overflow,
+                                               uint32_t* wdbg) {
     const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
     const float a = dot(r.d, r.d);
     const float ra = 1.0f / a;
@@ -1011,6 +1013,17 @@ __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* n
     while (true) {
         if (++guard > 8192u) {
             overflow = 1;
+            // (RTOW_WIDE_DEBUG: the first lane that trips records its ray and state)
+            if (wdbg && atomicCAS(wdbg, 0u, 1u) == 0u) {
+                const float v[8] = {r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.time, tmin};
+                for (int k = 0; k < 8; k++) wdbg[1 + k] = __float_as_uint(v[k]);
+                wdbg[9] = cur;
+                wdbg[10] = (uint32_t)sp;
+                for (int k = 0; k < 32; k++) wdbg[11 + k] = stk[k * BS];
+                wdbg[43] = root;
+                wdbg[44] = (uint32_t)(nodes == nullptr);
+                for (int k = 0; k < 32; k++) wdbg[45 + k] = reinterpret_cast<const uint32_t*>(nodes + (root & 0x7FFFu))[k];
+            }
             break;
         }
         const float4* np = reinterpret_cast<const float4*>(nodes + (cur & 0x7FFFu));
@@ -2543,9 +2556,9 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                                 : trace_wide_spec<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec,
                                                                     overflow);
                 else if (fast)
-                    prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow);
+                    prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow, P.wdbg);
                 else
-                    prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow);
+                    prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow, P.wdbg);
             } else {
                 if (fast)
                     prim = trace_simple<STACK, BS, PROF, true>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
@@ -4780,6 +4793,7 @@ struct rtow_context {
     int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
     uint32_t wide = 0;  // RTOW_WIDE=k: simple scenes over a 4-wide tree with leaves of <= k spheres (MODE 7)
     uint32_t spec = 0;  // RTOW_SPEC=n: MODE 7 with postponed leaves (trace_wide_spec), leaf pass below n inner lanes
+    uint32_t* wdbg = nullptr;  // RTOW_WIDE_DEBUG: 128 words (trace_wide's guard trip), printed to stderr
     // rtow_debug_trace_sample (a render with the segment-recording kernel)
     float* dbg_out = nullptr;
     uint32_t dbg_col = 0, dbg_row = 0, dbg_sample = 0, dbg_max = 0;
@@ -4994,6 +5008,7 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     const int rc = planParams(c->cus, c->auto_spc, p, P);
     if (rc) return rc;
     P.spec = c->spec;
+    P.wdbg = c->wdbg;
     P.dbg_out = c->dbg_out;
     P.dbg_col = c->dbg_col;
     P.dbg_row = c->dbg_row;
@@ -5095,6 +5110,20 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
             std::fprintf(stderr, "rtow-profile: Box leaf scans in node steps %.3f per ray, %.1f lanes per wave scan\n",
                          (double)host_ctr[34] / std::max(1ull, host_ctr[0]), (double)host_ctr[34] / host_ctr[35]);
     }
+    if (host_ctr[1] && c->wdbg) {
+        uint32_t w[128];
+        if (hipMemcpy(w, c->wdbg, sizeof w, hipMemcpyDeviceToHost) == hipSuccess && w[0]) {
+            float v[8];
+            std::memcpy(v, w + 1, sizeof v);
+            std::fprintf(stderr, "rtow-wide-debug: o %a %a %a d %a %a %a time %a tmin %a cur %08x sp %u root %08x\n", v[0],
+                         v[1], v[2], v[3], v[4], v[5], v[6], v[7], w[9], w[10], w[43]);
+            std::fprintf(stderr, "rtow-wide-debug: stack");
+            for (int k = 0; k < 32; k++) std::fprintf(stderr, " %04x", w[11 + k] & 0xFFFFu);
+            std::fprintf(stderr, "\nrtow-wide-debug: root node words");
+            for (int k = 0; k < 32; k++) std::fprintf(stderr, " %08x", w[45 + k]);
+            std::fprintf(stderr, "\n");
+        }
+    }
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
     if (host_ctr[13])
         return set_error(RTOW_E_UNSUPPORTED, "a chunk of samples summed to NaN or infinity");
@@ -5162,6 +5191,10 @@ int rtow_context_create(int device, rtow_context** out) {
     if (const char* tr = std::getenv("RTOW_BVH")) c->tree = std::string(tr) == "ref" ? RTOW_TREE_REFERENCE : RTOW_TREE_SAH;
     if (const char* wd = std::getenv("RTOW_WIDE")) c->wide = (uint32_t)std::max(0, std::atoi(wd));
     if (const char* sv = std::getenv("RTOW_SPEC")) c->spec = (uint32_t)std::max(0, std::atoi(sv));
+    if (std::getenv("RTOW_WIDE_DEBUG")) {
+        if ((e = hipMalloc(&c->wdbg, 512)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+        if ((e = hipMemset(c->wdbg, 0, 512)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
+    }
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
@@ -5181,6 +5214,7 @@ int rtow_context_destroy(rtow_context* c) {
     if (c->d_xframes) (void)hipFree(c->d_xframes);
     if (c->d_fb) (void)hipFree(c->d_fb);
     if (c->d_accum) (void)hipFree(c->d_accum);
+    if (c->wdbg) (void)hipFree(c->wdbg);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
