@@ -183,7 +183,6 @@ struct DevParams {
     struct XFrame* xframes;  // xhit's call frames: DevScene::xdepth x xstride (the grid's threads)
     uint32_t xstride;
     uint32_t spec;  // MODE 7: postponed leaves (trace_wide_spec) below this many lanes with inner work; 0: off
-    uint32_t* wdbg;  // MODE 7 debugging (RTOW_WIDE_DEBUG): the first guard trip's ray and state
 };
 
 struct Rec {
@@ -989,41 +988,34 @@ __device__ __forceinline__ uint32_t trace_simple(const DevScene& S, const DNode*
 // whose node has a sphere slot).
 // Node references are 16 bits (WIDE_LEAF | node index; WIDE_NONE: none) and
 // the stack holds them as 16-bit entries: the lane's LDS column of STACK words
-// holds 2 STACK entries (an inner step can push three).
+// holds 2 STACK entries (an inner step can push three), entry e in the low or
+// high half of the column's word e / 2 -- inside the lane's own 32-bit column,
+// which other waves' 32-bit uses of the stack region (wave_turbulence's
+// scratch) never touch (a 16-bit column of its own would overlap theirs).
+__device__ __forceinline__ uint16_t* wide_slot(uint32_t* col, int e, int bs) {
+    return reinterpret_cast<uint16_t*>(col + (e >> 1) * bs) + (e & 1);
+}
 constexpr uint32_t WIDE_LEAF = 0x8000u, WIDE_NONE = 0xFFFFu;
 template <int STACK, int BS, bool FAST>
 __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* nodes, uint32_t root, const Ray& r,
-                                               float tmin, float& bt, uint32_t* stk32, uint32_t& overflow,
-                                               uint32_t* wdbg) {
+                                               float tmin, float& bt, uint32_t* stk32, uint32_t& overflow) {
     const SlabRayF q = slab_ray_f(add(r.o, f3(S.tshift[0], S.tshift[1], S.tshift[2])), r.d);
     const float a = dot(r.d, r.d);
     const float ra = 1.0f / a;
     const float time = r.time;
     const uint32_t NONE = WIDE_NONE;
-    // the lane's column: stk32 = stack base + lane; 16-bit entry e at [e * BS]
-    uint16_t* const stk = reinterpret_cast<uint16_t*>(stk32 - (threadIdx.x)) + threadIdx.x;
+    // the lane's column: stk32 = stack base + lane (wide_slot)
     unsigned long long rkey = (unsigned long long)__float_as_uint(bt) << 32 | (uint32_t)~mkref(DK_NONE, 0);
     // (clamped: an empty child slot's box has every plane at +inf, which no
     // ray reaches within a finite bound -- see buildWide)
     float btc = fminf(cull_bound(bt) + q.werr, FLT_MAX);
-    stk[0] = (uint16_t)NONE;  // sentinel (trace_simple)
+    *wide_slot(stk32, 0, BS) = (uint16_t)NONE;  // sentinel (trace_simple)
     int sp = 1;
     uint32_t cur = root;
     uint32_t guard = 0;  // (experiment: a step bound that can only fail loudly)
     while (true) {
         if (++guard > 8192u) {
             overflow = 1;
-            // (RTOW_WIDE_DEBUG: the first lane that trips records its ray and state)
-            if (wdbg && atomicCAS(wdbg, 0u, 1u) == 0u) {
-                const float v[8] = {r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.time, tmin};
-                for (int k = 0; k < 8; k++) wdbg[1 + k] = __float_as_uint(v[k]);
-                wdbg[9] = cur;
-                wdbg[10] = (uint32_t)sp;
-                for (int k = 0; k < 32; k++) wdbg[11 + k] = stk[k * BS];
-                wdbg[43] = root;
-                wdbg[44] = (uint32_t)(nodes == nullptr);
-                for (int k = 0; k < 32; k++) wdbg[45 + k] = reinterpret_cast<const uint32_t*>(nodes + (root & 0x7FFFu))[k];
-            }
             break;
         }
         const float4* np = reinterpret_cast<const float4*>(nodes + (cur & 0x7FFFu));
@@ -1055,9 +1047,9 @@ __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* n
             cs(d1, r1, d2, r2);
             // far to near onto the stack, the nearest next (an empty slot's
             // box is empty: never hit)
-            if (d3 < INF) stk[sp++ * BS] = (uint16_t)r3;
-            if (d2 < INF) stk[sp++ * BS] = (uint16_t)r2;
-            if (d1 < INF) stk[sp++ * BS] = (uint16_t)r1;
+            if (d3 < INF) *wide_slot(stk32, sp++, BS) = (uint16_t)r3;
+            if (d2 < INF) *wide_slot(stk32, sp++, BS) = (uint16_t)r2;
+            if (d1 < INF) *wide_slot(stk32, sp++, BS) = (uint16_t)r1;
             nxt = d0 < INF ? r0 : NONE;
         } else {
             const float4 s0 = np[0], s1 = np[1], s2 = np[2], s3 = np[3], m0 = np[4], m1 = np[5], m2 = np[6];
@@ -1079,7 +1071,7 @@ __device__ __forceinline__ uint32_t trace_wide(const DevScene& S, const DWide* n
             }
         }
         if (nxt == NONE) {  // pop (entry 0: the sentinel)
-            nxt = stk[(sp - 1) * BS];
+            nxt = *wide_slot(stk32, sp - 1, BS);
             sp = max(sp - 1, 1);
         }
         if (nxt == NONE) break;
@@ -1106,10 +1098,9 @@ __device__ __forceinline__ uint32_t trace_wide_spec(const DevScene& S, const DWi
     const float ra = 1.0f / a;
     const float time = r.time;
     const uint32_t NONE = WIDE_NONE;
-    uint16_t* const stk = reinterpret_cast<uint16_t*>(stk32 - (threadIdx.x)) + threadIdx.x;
     unsigned long long rkey = (unsigned long long)__float_as_uint(bt) << 32 | (uint32_t)~mkref(DK_NONE, 0);
     float btc = fminf(cull_bound(bt) + q.werr, FLT_MAX);
-    stk[0] = (uint16_t)NONE;
+    *wide_slot(stk32, 0, BS) = (uint16_t)NONE;
     int sp = 1;
     uint32_t cur = root, parked = NONE;
     uint32_t guard = 0;
@@ -1120,7 +1111,7 @@ __device__ __forceinline__ uint32_t trace_wide_spec(const DevScene& S, const DWi
         }
         if (cur != NONE && (cur & WIDE_LEAF) && parked == NONE) {  // park the leaf, go on with the stack
             parked = cur;
-            cur = stk[(sp - 1) * BS];
+            cur = *wide_slot(stk32, sp - 1, BS);
             sp = max(sp - 1, 1);
         }
         const bool inner = cur != NONE && !(cur & WIDE_LEAF);
@@ -1176,13 +1167,13 @@ __device__ __forceinline__ uint32_t trace_wide_spec(const DevScene& S, const DWi
             cs(d0, r0, d2, r2);
             cs(d1, r1, d3, r3);
             cs(d1, r1, d2, r2);
-            if (d3 < INF) stk[sp++ * BS] = (uint16_t)r3;
-            if (d2 < INF) stk[sp++ * BS] = (uint16_t)r2;
-            if (d1 < INF) stk[sp++ * BS] = (uint16_t)r1;
+            if (d3 < INF) *wide_slot(stk32, sp++, BS) = (uint16_t)r3;
+            if (d2 < INF) *wide_slot(stk32, sp++, BS) = (uint16_t)r2;
+            if (d1 < INF) *wide_slot(stk32, sp++, BS) = (uint16_t)r1;
             if (d0 < INF) {
                 cur = r0;
             } else {
-                cur = stk[(sp - 1) * BS];
+                cur = *wide_slot(stk32, sp - 1, BS);
                 sp = max(sp - 1, 1);
             }
         }
@@ -2556,9 +2547,9 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                                 : trace_wide_spec<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, P.spec,
                                                                     overflow);
                 else if (fast)
-                    prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow, P.wdbg);
+                    prim = trace_wide<STACK, BS, true>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow);
                 else
-                    prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow, P.wdbg);
+                    prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow);
             } else {
                 if (fast)
                     prim = trace_simple<STACK, BS, PROF, true>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
@@ -2832,8 +2823,9 @@ __global__ void assemble_lin_kernel(uint32_t W, uint32_t H, uint32_t world, uint
 #define RTOW_KLIST_G(X, M)                                                                         \
     RTOW_K_COMMON(X, M, 16) RTOW_K_PROF(X, M, 16) RTOW_K_COMMON(X, M, 20) RTOW_K_PROF(X, M, 20)   \
     RTOW_K_COMMON(X, M, 32) RTOW_K_PROF(X, M, 32) RTOW_K_DEEP(X, M)
-#define RTOW_K_HOT(X) X(0, 16, 4, false, 512, true, false) X(7, 16, 4, false, 512, true, false) \
-    X(7, 32, 4, false, 512, true, false)
+#define RTOW_K_HOT(X) X(0, 16, 4, false, 512, true, false)
+// the 4-wide tree (MODE 7, opt-in RTOW_WIDE: measured slower), out of the hot kernel's unit
+#define RTOW_KLIST_7(X) X(7, 16, 4, false, 512, true, false) X(7, 32, 4, false, 512, true, false)
 #define RTOW_KLIST_6(X) RTOW_K_COMMON(X, 6, 16) RTOW_K_PROF(X, 6, 16)
 #if defined(RTOW_TU_SIMPLE)
 #define RTOW_KX(M, S, W, P, B, L, D) template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
@@ -2844,6 +2836,8 @@ RTOW_K_HOT(RTOW_KX)
 RTOW_KLIST_0(RTOW_KX)
 #elif RTOW_TU_KERNELS == 6
 RTOW_KLIST_6(RTOW_KX)
+#elif RTOW_TU_KERNELS == 7
+RTOW_KLIST_7(RTOW_KX)
 #else
 RTOW_KLIST_G(RTOW_KX, RTOW_TU_KERNELS)
 #endif
@@ -2857,6 +2851,7 @@ RTOW_KLIST_G(RTOW_KX, 3)
 RTOW_KLIST_G(RTOW_KX, 4)
 RTOW_KLIST_G(RTOW_KX, 5)
 RTOW_KLIST_6(RTOW_KX)
+RTOW_KLIST_7(RTOW_KX)
 #endif
 #undef RTOW_KX
 
@@ -4793,7 +4788,6 @@ struct rtow_context {
     int tree = RTOW_TREE_SAH;  // rtow_context_set_tree / RTOW_BVH
     uint32_t wide = 0;  // RTOW_WIDE=k: simple scenes over a 4-wide tree with leaves of <= k spheres (MODE 7)
     uint32_t spec = 0;  // RTOW_SPEC=n: MODE 7 with postponed leaves (trace_wide_spec), leaf pass below n inner lanes
-    uint32_t* wdbg = nullptr;  // RTOW_WIDE_DEBUG: 128 words (trace_wide's guard trip), printed to stderr
     // rtow_debug_trace_sample (a render with the segment-recording kernel)
     float* dbg_out = nullptr;
     uint32_t dbg_col = 0, dbg_row = 0, dbg_sample = 0, dbg_max = 0;
@@ -5008,7 +5002,6 @@ int makeParams(const rtow_context* c, const rtow_params* p, DevParams& P) {
     const int rc = planParams(c->cus, c->auto_spc, p, P);
     if (rc) return rc;
     P.spec = c->spec;
-    P.wdbg = c->wdbg;
     P.dbg_out = c->dbg_out;
     P.dbg_col = c->dbg_col;
     P.dbg_row = c->dbg_row;
@@ -5110,20 +5103,6 @@ int renderCore(rtow_context* c, const rtow_camera* cam, const rtow_params* p, ui
             std::fprintf(stderr, "rtow-profile: Box leaf scans in node steps %.3f per ray, %.1f lanes per wave scan\n",
                          (double)host_ctr[34] / std::max(1ull, host_ctr[0]), (double)host_ctr[34] / host_ctr[35]);
     }
-    if (host_ctr[1] && c->wdbg) {
-        uint32_t w[128];
-        if (hipMemcpy(w, c->wdbg, sizeof w, hipMemcpyDeviceToHost) == hipSuccess && w[0]) {
-            float v[8];
-            std::memcpy(v, w + 1, sizeof v);
-            std::fprintf(stderr, "rtow-wide-debug: o %a %a %a d %a %a %a time %a tmin %a cur %08x sp %u root %08x\n", v[0],
-                         v[1], v[2], v[3], v[4], v[5], v[6], v[7], w[9], w[10], w[43]);
-            std::fprintf(stderr, "rtow-wide-debug: stack");
-            for (int k = 0; k < 32; k++) std::fprintf(stderr, " %04x", w[11 + k] & 0xFFFFu);
-            std::fprintf(stderr, "\nrtow-wide-debug: root node words");
-            for (int k = 0; k < 32; k++) std::fprintf(stderr, " %08x", w[45 + k]);
-            std::fprintf(stderr, "\n");
-        }
-    }
     if (host_ctr[1]) return set_error(RTOW_E_UNSUPPORTED, "traversal stack overflow (scene deeper than bound)");
     if (host_ctr[13])
         return set_error(RTOW_E_UNSUPPORTED, "a chunk of samples summed to NaN or infinity");
@@ -5191,10 +5170,6 @@ int rtow_context_create(int device, rtow_context** out) {
     if (const char* tr = std::getenv("RTOW_BVH")) c->tree = std::string(tr) == "ref" ? RTOW_TREE_REFERENCE : RTOW_TREE_SAH;
     if (const char* wd = std::getenv("RTOW_WIDE")) c->wide = (uint32_t)std::max(0, std::atoi(wd));
     if (const char* sv = std::getenv("RTOW_SPEC")) c->spec = (uint32_t)std::max(0, std::atoi(sv));
-    if (std::getenv("RTOW_WIDE_DEBUG")) {
-        if ((e = hipMalloc(&c->wdbg, 512)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
-        if ((e = hipMemset(c->wdbg, 0, 512)) != hipSuccess) return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
-    }
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));
     for (auto& ev : c->ev)
@@ -5214,7 +5189,6 @@ int rtow_context_destroy(rtow_context* c) {
     if (c->d_xframes) (void)hipFree(c->d_xframes);
     if (c->d_fb) (void)hipFree(c->d_fb);
     if (c->d_accum) (void)hipFree(c->d_accum);
-    if (c->wdbg) (void)hipFree(c->wdbg);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
