@@ -1189,7 +1189,13 @@ __device__ __forceinline__ uint32_t trace_wide_spec(const DevScene& S, const DWi
 // register stack top, no kind dispatch.  `r` is the ray in the spheres' frame,
 // inv its reciprocals, a = dot(d, d), ra = 1 / a; bt / best the record so far
 // (the list's closest hit), updated with the reference's tie rule (tie keys).
-template <int STACK>
+// LEAVES (TOP_DTREE: a BvhNode tree without instances, lists or media below
+// it, final_ned's first tree of ground Boxes, light and spheres): a slot may
+// also hold a Box (DK_BOX6), a rectangle or a sphere that is not inlined
+// (DK_MSPHERE); its box hit, it is tested right there -- the same tests and
+// tie keys as the general traversal's visit of that leaf (traverse), without
+// the visit.
+template <int STACK, bool LEAVES = false>
 __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, const Ray& r, const F3& inv, float a,
                                              float ra, float tmin, float& bt, uint32_t& best, uint32_t* stk,
                                              uint32_t& overflow) {
@@ -1227,6 +1233,32 @@ __device__ __forceinline__ bool trace_dnodes(const DevScene& S, uint32_t root, c
             }
         } else {
             ha = slab(a0.x, a0.w, a0.y, a1.x, a0.z, a1.y, q, tmin, btc, ta);
+        }
+        if constexpr (LEAVES) {
+            uint32_t l0 = hb && (refb >> KIND_SHIFT) != DK_BVH ? refb : 0u;
+            uint32_t l1 = ha && (refa >> KIND_SHIFT) != DK_BVH ? refa : 0u;
+            if (l0) hb = false;
+            if (l1) ha = false;
+            if (!l0) l0 = l1, l1 = 0u;
+            if (l0) {
+                do {  // one copy of the leaf tests for both slots
+                    const uint32_t lk = l0 >> KIND_SHIFT, li = l0 & INDEX_MASK;
+                    float t;
+                    if (lk == DK_BOX6) {
+                        if (box6_scan(S, li, r, q.inv, tmin, bt, best)) found = true;
+                    } else if (lk == DK_RECT) {
+                        if (rect_t(S.rect[li], r, q.inv, tmin, bt, t) && take_hit(S, t, bt, best, l0)) found = true;
+                    } else {  // DK_MSPHERE
+                        const Sph s = load_sph(S.sph + li);
+                        const F3 c = S.unit_time ? sph_center<true>(s, r.time) : sph_center<false>(s, r.time);
+                        if (sph_root(c, s.r * s.r, r, a, ra, tmin, t) && take_hit(S, t, bt, best, mkref(DK_SPHERE, li)))
+                            found = true;
+                    }
+                    l0 = l1;
+                    l1 = 0u;
+                } while (l0);
+                btc = cull_bound(bt);
+            }
         }
         const bool afirst = ta <= tb;
         const bool both = ha && hb;
@@ -1646,6 +1678,8 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             }
         } else if (kind == TOP_SPHERES) {
             trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
+        } else if (kind == TOP_DTREE) {
+            trace_dnodes<STACK, true>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
         } else if (kind == TOP_SPHERE) {
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
@@ -3959,6 +3993,33 @@ bool sphereNodesOnly(const HostLayout& L, uint32_t i, int depth = 0) {
     return true;
 }
 
+// every slot of the DNode twins reachable from node i is an inner node or a
+// leaf trace_dnodes<LEAVES> tests in place (TOP_DTREE)
+bool dtreeNodesOnly(const HostLayout& L, uint32_t i, int depth = 0) {
+    if (i >= L.node.size() || depth > 4096) return false;
+    const DNode& d = L.node[i];
+    for (uint32_t ref : {d.ref_a, d.ref_b}) {
+        const uint32_t k = ref >> KIND_SHIFT;
+        if (k == DK_BVH) {
+            if (!dtreeNodesOnly(L, ref & INDEX_MASK, depth + 1)) return false;
+        } else if (k != DK_SPHERE && k != DK_MSPHERE && k != DK_BOX6 && k != DK_RECT) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// true when `ref` is a BvhNode whose leaves are only spheres, rectangles and
+// Boxes (no instance, list or medium below it): its DNode twin holds only the
+// slots dtreeNodesOnly accepts (buildGeneralNodes)
+bool dtreeLeaves(const HostLayout& L, uint32_t ref, int depth = 0) {
+    const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
+    if (depth > 4096) return false;
+    if (kind == DK_BVH) return dtreeLeaves(L, L.bvh[idx].left, depth + 1) && dtreeLeaves(L, L.bvh[idx].right, depth + 1);
+    if (kind == DK_SPHERE || kind == DK_MSPHERE || kind == DK_RECT) return true;
+    return kind == DK_RECTS && L.list[idx].box6 != 0;
+}
+
 // true when everything below `ref` is BvhNodes and spheres
 bool onlyBvhSpheres(const HostLayout& L, uint32_t ref, int depth = 0) {
     const uint32_t kind = ref >> KIND_SHIFT, idx = ref & INDEX_MASK;
@@ -4408,6 +4469,9 @@ struct ProgramBuilder {
 // list (empty otherwise)
 void buildTop(HostLayout& L) {
     L.top.clear();
+    // RTOW_DTREE=0: such trees go to the general traversal (TOP_GENERIC) instead (A/B)
+    const char* dt = std::getenv("RTOW_DTREE");
+    const bool dtree = !dt || std::atoi(dt) != 0;
     std::vector<uint32_t> path;
     uint32_t ref = L.root;
     for (int guard = 0; guard < 64; guard++) {
@@ -4456,6 +4520,8 @@ void buildTop(HostLayout& L) {
             uint32_t s0 = leaf;  // any leaf sphere gives the chain of the frame they share
             while ((s0 >> KIND_SHIFT) == DK_BVH) s0 = L.bvh[s0 & INDEX_MASK].left;
             t = DTop{TOP_SPHERES, i, 0, L.sph[s0 & INDEX_MASK].chain};
+        } else if (k == DK_BVH && leaf == item && dtree && dtreeLeaves(L, item)) {
+            t = DTop{TOP_DTREE, i, 0, list_chain};  // (the leaves sit in the list's frame: no instance below)
         }
         L.top.push_back(t);
     }
@@ -4734,8 +4800,9 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH, ui
         buildGeneralNodes(L);  // DNode twins of the SAH trees, or of the reference's own (RTOW_TREE_REFERENCE)
         // trace_dnodes (TOP_SPHERES) takes every non-sphere slot for an inner node
         for (const DTop& t : L.top)
-            if ((t.kind & TOP_KIND_MASK) == TOP_SPHERES && !sphereNodesOnly(L, t.a))
-                return set_error(RTOW_E_INVALID, "internal: TOP_SPHERES tree with a slot that is neither a sphere nor a node");
+            if (((t.kind & TOP_KIND_MASK) == TOP_SPHERES && !sphereNodesOnly(L, t.a)) ||
+                ((t.kind & TOP_KIND_MASK) == TOP_DTREE && !dtreeNodesOnly(L, t.a)))
+                return set_error(RTOW_E_INVALID, "internal: TOP_SPHERES / TOP_DTREE tree with a slot its loop does not test");
     }
     if (exact) {
         const int rc = buildExact(s, L);

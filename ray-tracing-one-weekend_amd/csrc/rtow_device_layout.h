@@ -200,13 +200,23 @@ struct alignas(16) DProg {  // 32 B; lo/hi read as ref_aabb_hit's (min xyz, -, m
 // goes to the general traversal -- except a chain of instances over a BvhNode
 // of unit-time spheres only (final_ned's cloud, Translate(RotateY(BvhNode of
 // 1000 spheres))): TOP_SPHERES runs its DNode tree in a loop of its own
-// (trace_dnodes) in the leaves' frame, entered once per ray.
-enum : uint32_t { TOP_GENERIC = 0, TOP_RECTS = 1, TOP_SPHERE = 2, TOP_MEDIUM = 3, TOP_BOX6 = 4, TOP_SPHERES = 5 };
+// (trace_dnodes) in the leaves' frame, entered once per ray; and so does a
+// BvhNode whose leaves are only spheres, rectangles and Boxes, with no
+// instance, list or medium below it (TOP_DTREE: final_ned's first tree).
+enum : uint32_t {
+    TOP_GENERIC = 0,
+    TOP_RECTS = 1,
+    TOP_SPHERE = 2,
+    TOP_MEDIUM = 3,
+    TOP_BOX6 = 4,
+    TOP_SPHERES = 5,
+    TOP_DTREE = 6
+};
 // DTop::kind flags above the kind (buildTop): the item's frame differs from
 // the previous in-place item's (the scan recomputes its ray), and so does the
 // ray's direction there (it recomputes 1/d and dot(d, d) too)
 enum : uint32_t { TOP_KIND_MASK = 255u, TOP_NEWCHAIN = 1u << 8, TOP_NEWDIR = 1u << 9 };
-// BOX6: a = box6 index; SPHERES: a = the DNode index of the BvhNode
+// BOX6: a = box6 index; SPHERES, DTREE: a = the DNode index of the BvhNode
 struct alignas(16) DTop {  // 16 B
     uint32_t kind;
     uint32_t a;      // GENERIC: item ref; RECTS: first rectangle; SPHERE: sphere; MEDIUM: medium

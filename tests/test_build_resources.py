@@ -27,8 +27,11 @@ LIB = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "librtow_hip.so")
 # (xhit's call frames live in a global buffer, DevParams::xframes, not in
 # scratch: a private array sized every wave's scratch for it.)
 # (MODE 4, used by no BASELINE config: 12 B in round 3, 24 since the uniform scene
-# records are scalar loads -- SGPR pressure)
-SCRATCH_BOUND = {0: 0, 2: 0, 4: 24, 3: 96, 5: 0, 6: 0, 7: 24}  # 7: the 4-wide tree (RTOW_WIDE, experiment)
+# records are scalar loads -- SGPR pressure; MODE 2 and MODE 5's STACK 20 / 32
+# variants: 12 / 8 B since trace_dnodes tests leaf slots in place, TOP_DTREE --
+# cornell unchanged, A/B; the config-5 kernel, MODE 5 at STACK 16, has none:
+# test_config5_kernel_has_no_scratch)
+SCRATCH_BOUND = {0: 0, 2: 12, 4: 24, 3: 96, 5: 8, 6: 0, 7: 24}  # 7: the 4-wide tree (RTOW_WIDE, experiment)
 
 
 @pytest.fixture(scope="module")
@@ -50,6 +53,13 @@ def test_bench_kernel_has_no_scratch(kernels):
     assert len(hot) == 1
     assert hot[0]["scratch"] == 0 and hot[0]["vgpr_spill"] == 0
     assert hot[0]["vgpr"] <= 128  # 4 waves per SIMD
+
+
+def test_config5_kernel_has_no_scratch(kernels):
+    k5 = [k for k in kernels if codeobj.demangled_params(k["name"]) ==
+          {"MODE": 5, "STACK": 16, "WAVES": 4, "PROF": 0, "BS": 256, "LDSN": 0, "DBG": 0}]
+    assert len(k5) == 1
+    assert k5[0]["scratch"] == 0 and k5[0]["vgpr_spill"] == 0
 
 
 def test_default_kernels_scratch_bounded(kernels):

@@ -109,3 +109,19 @@ def _save(s, tmp_path):
     p = str(tmp_path / "s.scn")
     s.save(p)
     return p
+
+
+@pytest.mark.parametrize("dtree,kind0", [("1", 6), ("0", 0)])
+def test_final_scene_top_level_items(dtree, kind0):
+    """final_ned's top-level scan (buildTop, printed by RTOW_LAYOUT_INFO): the
+    first tree (ground Boxes, light, spheres) runs in trace_dnodes' loop with
+    leaf slots (TOP_DTREE = 6) unless RTOW_DTREE=0 sends it to the general
+    traversal (TOP_GENERIC = 0); two media (3), two spheres (2), the cloud (5)."""
+    import subprocess
+    import sys
+    code = ("import rtow; rtow.Scene.build('final_ned', n=100, image='synthetic').check()")
+    env = dict(os.environ, RTOW_LAYOUT_INFO="1", RTOW_DTREE=dtree)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(rtow.__file__)).stderr
+    kinds = [int(l.split(" kind ")[1].split()[0]) for l in out.splitlines() if l.startswith("rtow-layout: top[")]
+    assert kinds == [kind0, 3, 3, 2, 2, 5]
