@@ -196,6 +196,7 @@ def cpu_baseline(scene, cam, args, threads):
             "msample_per_s": round(c.samples / dt / 1e6, 4), "seconds": round(dt, 2),
             "sample": sample + ", oracle/librtow_oracle.so"}
     base = port
+    print(f"cpu_baseline: oracle {dt:.1f} s; the reference's own code next", file=sys.stderr, flush=True)
     ref = reference_run(pix, args, threads) if args.cpu_kind != "port" else None
     if ref is not None:
         rs, checksum = ref
@@ -205,6 +206,7 @@ def cpu_baseline(scene, cam, args, threads):
                 "sample": sample + ", oracle/_ref/ref_harness (the reference's headers); rays counted by the oracle",
                 "same_result_as_oracle": bool(abs(checksum - osum) <= 1e-6 * max(1.0, abs(osum))),
                 "port": {k: port[k] for k in ("value", "msample_per_s", "seconds")}}
+        print(f"cpu_baseline: reference {rs:.1f} s; the reference as written next", file=sys.stderr, flush=True)
         racy = reference_run(pix, args, threads, racy=True)
         if racy is not None:
             # its paths differ from the seeded ones (other random numbers):

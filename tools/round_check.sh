@@ -19,7 +19,7 @@ if [[ $STEPS == *profile* ]]; then
 fi
 if [[ $STEPS == *general* ]]; then
   for w in cornell cornell_smoke; do
-    bash tools/profile_bench.sh ${TAG}_$w --workload $w --cpu-pixels 40000 > gpurun_out/profile_${TAG}_$w.log 2>&1 || exit $?
+    bash tools/profile_bench.sh ${TAG}_$w --workload $w --cpu-pixels 16000 > gpurun_out/profile_${TAG}_$w.log 2>&1 || exit $?
   done
   # config 5 at its full 4096x4096 frame, 256 spp per launch (VALU per ray does not depend on spp)
   bash tools/profile_bench.sh ${TAG}_final_ned --workload final_ned --spp 256 --cpu-pixels 8000 --cpu-spp 512 \
