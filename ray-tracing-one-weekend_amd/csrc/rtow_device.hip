@@ -312,6 +312,17 @@ __device__ __forceinline__ SlabRay slab_ray_inv(F3 o, F3 inv) {
 }
 __device__ __forceinline__ SlabRay slab_ray(const Ray& r) { return slab_ray_inv(r.o, inv_dir(r.d)); }
 
+// min(a, b) as the bare v_min_f32.  fminf() makes the compiler canonicalise
+// an operand it cannot prove canonical (the culling bound is a loop-carried
+// select: one extra v_max_f32 per slab test).  The slab tests' operands are
+// never signalling NaNs (a quiet NaN from (x - o) * inf gives the other
+// operand either way), so the result is fminf's.
+__device__ __forceinline__ float min_hw(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // Conservative slab test for culling (never the reference's own AABB::hit,
 // whose divisions only decide WHICH subtrees it visits, not the result).
 // The box's exit is widened by 2^-9 relative (see below);
@@ -331,7 +342,7 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
     // keeps it.  Widened by 2^-19, 11 pixels of final_ned at 1024^2 x 512 spp
     // differed from the oracle by > 1e-6; by 2^-13 or 2^-9, 2 (the same two
     // in both: transcendentals), at no measurable cost (tools/diverge.py).
-    const float tf = fminf(ex * 1.001953125f, tmax_c);
+    const float tf = min_hw(ex * 1.001953125f, tmax_c);
     tnear = tn;
     return tn <= tf;
 }
@@ -366,7 +377,7 @@ __device__ __forceinline__ bool slab_f(float x0, float x1, float y0, float y1, f
     const float tz0 = fmaf(z0, q.inv.z, -q.oi.z), tz1 = fmaf(z1, q.inv.z, -q.oi.z);
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
     const float ex = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-    const float tf = fminf(fmaf(ex, 1.001953125f, q.werr), tmax_c);  // see slab()
+    const float tf = min_hw(fmaf(ex, 1.001953125f, q.werr), tmax_c);  // see slab()
     tnear = tn;
     return tn <= tf;
 }
@@ -700,6 +711,121 @@ __device__ __forceinline__ bool box6_nearest(const DevScene& S, uint32_t bi, con
     if (rect_t_ax<0, 1, 2>(lo.y, hi.y, lo.z, hi.z, hi.x, r, inv, lo_t, near, t)) near = t, f = true;
     if (rect_t_ax<0, 1, 2>(lo.y, hi.y, lo.z, hi.z, lo.x, r, inv, lo_t, near, t)) near = t, f = true;
     return f;
+}
+
+// TOP_GRID (MODE 8): the Boxes of a grid of columns (DGrid), walked along the
+// ray: rows along v in the ray's v order, within a row the cells along u in
+// its u order.  Every cell is widened by G.margin (2^-10 of a cell, hundreds
+// of ulps of the scene's coordinates), and every t bound computed here by a
+// further 2^-18 relative, so the walk reaches every Box whose six-side scan
+// could yield a hit in [tmin, bt]: such a hit lies on the Box's surface up to
+// the rectangle tests' rounding, i.e. inside the widened column, at a height
+// inside the widened [hlo, hhi], at a t inside the widened bounds.  A cell
+// is scanned when the ray, over the cell's t interval, passes at a height the
+// cell's Box spans; the scan is box6_scan itself (the tree's leaf test:
+// same rectangle tests, same interval shrinking, same tie keys), so the record
+// is the tree's -- the set of Boxes tested is a superset of those that can
+// win, as for any culled visit order (see "Exact ties in general scenes").
+// The walk stops at the first row (cell) that starts beyond the culling bound
+// of the record.  The scans are batched: each lane walks to its next cell to
+// scan, then the wave scans the cells it found together (the walk steps are
+// a few VALU, a scan six rectangle tests).
+// The band of the ray's t in which o + t d lies in [lo, hi], widened; a zero
+// (or denormal) d, whose 1/d is infinite: every t or none.
+__device__ __forceinline__ void grid_band(float lo, float hi, float o, float id, float& t0, float& t1) {
+    constexpr float REL = 0x1p-18f;
+    const float a = (lo - o) * id, b = (hi - o) * id;
+    const float n = fminf(a, b), f = fmaxf(a, b);
+    const bool flat = !(fabsf(id) < INFINITY);
+    const bool in = lo <= o && o <= hi;
+    t0 = flat ? (in ? -INFINITY : INFINITY) : n - fabsf(n) * REL;
+    t1 = flat ? (in ? INFINITY : -INFINITY) : f + fabsf(f) * REL;
+}
+__device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const Ray& r, const F3& inv, float tmin,
+                                          float& bt, uint32_t& best) {
+    constexpr float REL = 0x1p-18f;
+    const DGrid G = cld(S.grid + gi);
+    const uint32_t au = G.axes & 3u, av = (G.axes >> 2) & 3u, ah = (G.axes >> 4) & 3u;
+    const float ou = comp(r.o, au), ov = comp(r.o, av), oh = comp(r.o, ah);
+    const float du = comp(r.d, au), dv = comp(r.d, av), dh = comp(r.d, ah);
+    const float iu = comp(inv, au), iv = comp(inv, av), ih = comp(inv, ah);
+    const float D = G.margin;
+    // the grid's box, widened: the walk's t range [te, tx]
+    float u0, u1, v0, v1, h0, h1;
+    grid_band(G.u0 - D, G.u1 + D, ou, iu, u0, u1);
+    grid_band(G.v0 - D, G.v1 + D, ov, iv, v0, v1);
+    grid_band(G.hlo - D, G.hhi + D, oh, ih, h0, h1);
+    const float te = fmaxf(fmaxf(u0, v0), fmaxf(h0, tmin));
+    const float tx = fminf(fminf(u1, v1), h1);  // finite: d has a non-zero component
+    if (!(te <= fminf(tx, cull_bound(bt)))) return false;
+    // the rows the ray can meet, one more either side for the widening
+    const bool vflat = !(fabsf(iv) < INFINITY), uflat = !(fabsf(iu) < INFINITY);
+    const int sv = dv < 0.0f ? -1 : 1, su = du < 0.0f ? -1 : 1;
+    const float fnv = (float)(G.nv - 1u), fnu = (float)(G.nu - 1u);
+    auto row_of = [&](float t) {
+        const float v = fmaf(t, dv, ov);
+        return fminf(fmaxf(floorf((v - G.v0) * G.iwv), -1.0f), (float)G.nv);
+    };
+    int j = (int)fminf(fmaxf(row_of(te) - (float)sv, 0.0f), fnv);
+    const int jl = (int)fminf(fmaxf(row_of(tx) + (float)sv, 0.0f), fnv);
+    int nrows = (jl - j) * sv + 1;
+    int i = 0, ncells = 0, jr = 0;
+    float ra = 0.0f, rb = 0.0f;
+    bool found = false, live = nrows > 0;
+    while (live) {
+        uint32_t cand = ~0u;
+        while (true) {  // this lane's next cell to scan
+            const float bound = cull_bound(bt);
+            if (ncells <= 0) {
+                if (nrows <= 0) {
+                    live = false;
+                    break;
+                }
+                const float vlo = fmaf((float)j, G.wv, G.v0);
+                float t0, t1;
+                grid_band(vlo - D, vlo + G.wv + D, ov, iv, t0, t1);
+                jr = j;
+                j += sv;
+                nrows--;
+                if (t0 > bound && !vflat) {  // this row and the later ones lie beyond the record
+                    live = false;
+                    break;
+                }
+                ra = fmaxf(t0, te);
+                rb = fminf(fminf(t1, tx), bound);
+                if (!(ra <= rb)) continue;
+                // the row's cells: u over [ra, rb], widened
+                const float ua = fmaf(ra, du, ou), ub = fmaf(rb, du, ou);
+                const float ue = D + (fabsf(ou) + fmaxf(fabsf(ua), fabsf(ub))) * REL;
+                const float fa = floorf((fminf(ua, ub) - ue - G.u0) * G.iwu);
+                const float fb = floorf((fmaxf(ua, ub) + ue - G.u0) * G.iwu);
+                const int ia = (int)fminf(fmaxf(fa - 1.0f, 0.0f), fnu), ib = (int)fminf(fmaxf(fb + 1.0f, 0.0f), fnu);
+                i = su > 0 ? ia : ib;
+                ncells = ib - ia + 1;
+                continue;
+            }
+            const int ic = i;
+            i += su;
+            ncells--;
+            const float ulo = fmaf((float)ic, G.wu, G.u0);
+            float c0, c1;
+            grid_band(ulo - D, ulo + G.wu + D, ou, iu, c0, c1);
+            c0 = fmaxf(c0, ra);
+            c1 = fminf(fminf(c1, rb), bound);
+            if (!(c0 <= c1)) {
+                if (c0 > bound && !uflat) ncells = 0;  // the rest of the row lies beyond the record
+                continue;
+            }
+            const DGridCell C = S.gcell[G.cell0 + (uint32_t)jr * G.nu + (uint32_t)ic];
+            const float ha = fmaf(c0, dh, oh), hb = fmaf(c1, dh, oh);
+            const float he = D + (fabsf(oh) + fmaxf(fabsf(ha), fabsf(hb))) * REL;
+            if (fmaxf(ha, hb) + he < C.hlo || fminf(ha, hb) - he > C.hhi) continue;
+            cand = C.box6;
+            break;
+        }
+        if (cand != ~0u && box6_scan(S, cand, r, inv, tmin, bt, best)) found = true;
+    }
+    return found;
 }
 
 // Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
@@ -1581,7 +1707,8 @@ __device__ __forceinline__ bool traverse(const DevScene& S, uint32_t root, const
 // TOPMED: media as top-level items (TOP_MEDIUM).
 // PARK: the caller parked the sample's RNG key (COLD words 14, 15) and its
 // counter (16) in LDS; media draw through them (registers, see cold_words).
-template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false, bool PARK = false>
+// GRID: TOP_GRID items may occur (MODE 8).
+template <bool MEDIA, int STACK, bool ANYB, bool TOPMED, bool PROF = false, bool PARK = false, bool GRID = false>
 __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray, float tmin, uint32_t* stk, Rng& rng, Best& best,
                              uint32_t& overflow, Prof* prof = nullptr) {
     float bt = FLT_MAX;
@@ -1680,6 +1807,8 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             trace_dnodes<STACK>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
         } else if (kind == TOP_DTREE) {
             trace_dnodes<STACK, true>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
+        } else if (GRID && kind == TOP_GRID) {
+            grid_walk(S, T.a, r, inv, tmin, bt, bp);
         } else if (kind == TOP_SPHERE) {
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
@@ -2438,7 +2567,8 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // MODE: 0 simple scene (BvhNodes + unit-time spheres under a root instance
 // chain), 2 general scene, 3 general scene with media, 4 general scene with
 // media whose boundaries are spheres or Boxes (no nested general traversal),
-// 5 general scene whose media are all top-level items with such boundaries
+// 5 general scene whose media are all top-level items with such boundaries,
+// 8 the same with TOP_GRID items (grid_walk)
 // (asked by the top-level scan only: the general traversal carries no media)
 // All LDS is one dynamic region (16-B aligned carve, no static __shared__):
 // Perlin ranvec (4 KB) | perms (1 KB) | traversal stack STACK x BS words |
@@ -2449,7 +2579,7 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // counter there too, PARK_RNG): either way 4 blocks of 256 fit a CU's 160 KB.
 constexpr int cold_words(int STACK) { return STACK <= 16 ? 17 : 14; }
 template <int MODE, int STACK>
-constexpr bool park_rng() { return MODE == 5 && STACK <= 16; }
+constexpr bool park_rng() { return (MODE == 5 || MODE == 8) && STACK <= 16; }
 
 constexpr size_t lds_bytes(int STACK, int BS, uint32_t n_node, bool ldsn, bool general = false) {
     return 4096 + 1024 + (size_t)STACK * BS * 4 + (ldsn ? (size_t)n_node * sizeof(DNode) : 0) +
@@ -2634,8 +2764,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 rng.key = 0;
                 rng.ctr = 0;
             }
-            hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF, PARK>(S, ray, 0.001f, stk, rng,
-                                                                                             best, overflow, &prof);
+            hit = traverse_top<MODE == 3 || MODE == 4, STACK, MODE == 3, MODE >= 3, PROF, PARK, MODE == 8>(
+                S, ray, 0.001f, stk, rng, best, overflow, &prof);
             if constexpr (PARK) {
                 rng.key = (uint64_t)cold[15 * BS] << 32 | cold[14 * BS];
                 rng.ctr = cold[16 * BS];
@@ -2861,6 +2991,9 @@ __global__ void assemble_lin_kernel(uint32_t W, uint32_t H, uint32_t world, uint
 // the 4-wide tree (MODE 7, opt-in RTOW_WIDE: measured slower), out of the hot kernel's unit
 #define RTOW_KLIST_7(X) X(7, 16, 4, false, 512, true, false) X(7, 32, 4, false, 512, true, false)
 #define RTOW_KLIST_6(X) RTOW_K_COMMON(X, 6, 16) RTOW_K_PROF(X, 6, 16)
+// MODE 8 (TOP_GRID worlds): the stacks final_ned-like worlds need
+#define RTOW_KLIST_8(X) RTOW_K_COMMON(X, 8, 16) RTOW_K_PROF(X, 8, 16) RTOW_K_COMMON(X, 8, 20) RTOW_K_PROF(X, 8, 20) \
+    RTOW_K_COMMON(X, 8, 32) RTOW_K_PROF(X, 8, 32) RTOW_K_DEEP(X, 8)
 #if defined(RTOW_TU_SIMPLE)
 #define RTOW_KX(M, S, W, P, B, L, D) template __global__ void trace_kernel<M, S, W, P, B, L, D>(RTOW_KERNEL_ARGS);
 RTOW_K_HOT(RTOW_KX)
@@ -2872,6 +3005,8 @@ RTOW_KLIST_0(RTOW_KX)
 RTOW_KLIST_6(RTOW_KX)
 #elif RTOW_TU_KERNELS == 7
 RTOW_KLIST_7(RTOW_KX)
+#elif RTOW_TU_KERNELS == 8
+RTOW_KLIST_8(RTOW_KX)
 #else
 RTOW_KLIST_G(RTOW_KX, RTOW_TU_KERNELS)
 #endif
@@ -2886,6 +3021,7 @@ RTOW_KLIST_G(RTOW_KX, 4)
 RTOW_KLIST_G(RTOW_KX, 5)
 RTOW_KLIST_6(RTOW_KX)
 RTOW_KLIST_7(RTOW_KX)
+RTOW_KLIST_8(RTOW_KX)
 #endif
 #undef RTOW_KX
 
@@ -2948,6 +3084,10 @@ struct HostLayout {
     std::vector<float> abox;         // DevScene::abox
     std::vector<DProg> prog;         // DevScene::prog
     std::vector<DBox6> box6;         // DevScene::box6
+    std::vector<DGrid> grid;         // DevScene::grid (TOP_GRID)
+    std::vector<DGridCell> gcell;    // DevScene::gcell
+    std::unordered_map<uint32_t, uint32_t> grid_of;  // a grid's BvhNode ref -> its DGrid
+    uint32_t grid_top = 0;           // TOP_GRID items of the top-level list (DevScene::n_grid)
     float tshift[3] = {0.0f, 0.0f, 0.0f};  // DevScene::tshift
     // exact-order worlds (MODE 6, xhit): the raw scene graph
     bool exact = false;
@@ -3595,6 +3735,93 @@ struct GeneralSah {
         return onlyUnitSpheres(L.bvh[idx].left, depth + 1) && onlyUnitSpheres(L.bvh[idx].right, depth + 1);
     }
 
+    // A BvhNode whose leaves are Boxes (rectangle lists with a DBox6), all in
+    // one frame, that tile a regular grid of columns along two axes (one Box
+    // per cell, within a 2^-12 cell width of the cell; any extent along the
+    // third axis): its DGrid is registered (L.grid_of) and the item stays out
+    // of the run's tree, so the top-level scan can walk it as a grid
+    // (TOP_GRID).  final_ned's ground: 20 x 20 Boxes 100 wide, heights 1..101.
+    // RTOW_GRID=0: no grids (A/B).
+    bool gridItem(uint32_t ref) {
+        if ((ref >> KIND_SHIFT) != DK_BVH) return false;
+        if (L.grid_of.count(ref)) return true;
+        if (const char* e = std::getenv("RTOW_GRID"))
+            if (std::atoi(e) == 0) return false;
+        std::vector<GenLeaf> lv;
+        bool bounded = true;
+        genLeaves(L, ref, lv, bounded);
+        if (!bounded || lv.size() < 16) return false;
+        std::vector<uint32_t> bx(lv.size());
+        uint32_t chain = ~0u;
+        for (size_t q = 0; q < lv.size(); q++) {
+            const uint32_t r = lv[q].ref;
+            if ((r >> KIND_SHIFT) != DK_RECTS) return false;
+            const DList& l = L.list[r & INDEX_MASK];
+            if (!l.box6) return false;
+            for (uint32_t k = 0; k < l.count; k++) {
+                const uint32_t c = L.rect[l.first + k].chain;
+                if (chain == ~0u) chain = c;
+                if (c != chain) return false;
+            }
+            bx[q] = l.box6 - 1;
+        }
+        for (uint32_t ah = 0; ah < 3; ah++) {
+            const uint32_t au = ah == 0 ? 1u : 0u, av = ah == 2 ? 1u : 2u;
+            float u0 = FLT_MAX, v0 = FLT_MAX, u1 = -FLT_MAX, v1 = -FLT_MAX, hlo = FLT_MAX, hhi = -FLT_MAX;
+            for (uint32_t b : bx) {
+                const DBox6& q = L.box6[b];
+                u0 = std::min(u0, q.lo[au]), v0 = std::min(v0, q.lo[av]);
+                u1 = std::max(u1, q.hi[au]), v1 = std::max(v1, q.hi[av]);
+                hlo = std::min(hlo, q.lo[ah]), hhi = std::max(hhi, q.hi[ah]);
+            }
+            const DBox6& f = L.box6[bx[0]];
+            const double wu = (double)f.hi[au] - f.lo[au], wv = (double)f.hi[av] - f.lo[av];
+            if (!(wu > 0 && wv > 0)) continue;
+            const double nuf = std::round((u1 - (double)u0) / wu), nvf = std::round((v1 - (double)v0) / wv);
+            if (!(nuf >= 1 && nvf >= 1 && nuf * nvf == (double)bx.size())) continue;
+            const uint32_t nu = (uint32_t)nuf, nv = (uint32_t)nvf;
+            const double tol = std::max(wu, wv) * 0x1p-12;
+            std::vector<DGridCell> cells((size_t)nu * nv);
+            std::vector<char> seen((size_t)nu * nv, 0);
+            bool ok = true;
+            for (uint32_t b : bx) {
+                const DBox6& q = L.box6[b];
+                const double fi = std::round((q.lo[au] - (double)u0) / wu), fj = std::round((q.lo[av] - (double)v0) / wv);
+                if (!(fi >= 0 && fi < nu && fj >= 0 && fj < nv)) {
+                    ok = false;
+                    break;
+                }
+                const double cu = u0 + fi * wu, cv = v0 + fj * wv;
+                if (std::fabs(q.lo[au] - cu) > tol || std::fabs(q.hi[au] - (cu + wu)) > tol ||
+                    std::fabs(q.lo[av] - cv) > tol || std::fabs(q.hi[av] - (cv + wv)) > tol || !(q.lo[ah] <= q.hi[ah])) {
+                    ok = false;
+                    break;
+                }
+                const size_t c = (size_t)fj * nu + (size_t)fi;
+                if (seen[c]) {
+                    ok = false;
+                    break;
+                }
+                seen[c] = 1;
+                cells[c] = DGridCell{q.lo[ah], q.hi[ah], b, 0u};
+            }
+            if (!ok) continue;
+            DGrid g{};
+            g.u0 = u0, g.v0 = v0, g.wu = (float)wu, g.wv = (float)wv;
+            g.iwu = (float)(1.0 / wu), g.iwv = (float)(1.0 / wv);
+            g.hlo = hlo, g.hhi = hhi, g.u1 = u1, g.v1 = v1;
+            g.nu = nu, g.nv = nv;
+            g.axes = au | av << 2 | ah << 4;
+            g.cell0 = (uint32_t)L.gcell.size();
+            g.margin = (float)(std::max(wu, wv) * 0x1p-10);  // 2^2 x the tolerance above
+            L.gcell.insert(L.gcell.end(), cells.begin(), cells.end());
+            L.grid_of[ref] = (uint32_t)L.grid.size();
+            L.grid.push_back(g);
+            return true;
+        }
+        return false;
+    }
+
     void treeRuns(const DList& l) {
         std::vector<uint32_t> items(L.refs.begin() + l.first, L.refs.begin() + l.first + l.count), out;
         size_t j = 0;
@@ -3605,7 +3832,7 @@ struct GeneralSah {
             for (; k < items.size(); k++) {
                 GenLeaf g;
                 if (hasMedium(items[k]) || !bounds(items[k], g.mn, g.mx)) break;
-                if (sphereInstance(items[k])) {
+                if (sphereInstance(items[k]) || gridItem(items[k])) {
                     alone.push_back(items[k]);
                     continue;
                 }
@@ -4494,8 +4721,10 @@ void buildTop(HostLayout& L) {
     }
     if (list_chain == ~0u) return;
     const DList l = L.list[ref & INDEX_MASK];
+    std::vector<uint32_t> items;
     for (uint32_t j = 0; j < l.count; j++) {
         const uint32_t item = L.refs[l.first + j];
+        items.push_back(item);
         uint32_t leaf = item;
         for (int guard = 0; guard < 64; guard++) {
             const uint32_t k = leaf >> KIND_SHIFT;
@@ -4520,10 +4749,35 @@ void buildTop(HostLayout& L) {
             uint32_t s0 = leaf;  // any leaf sphere gives the chain of the frame they share
             while ((s0 >> KIND_SHIFT) == DK_BVH) s0 = L.bvh[s0 & INDEX_MASK].left;
             t = DTop{TOP_SPHERES, i, 0, L.sph[s0 & INDEX_MASK].chain};
+        } else if (k == DK_BVH && leaf == item && L.grid_of.count(item)) {
+            const uint32_t g = L.grid_of[item];  // (the Boxes' frame: their sides' chain)
+            t = DTop{TOP_GRID, g, 0, L.rect[L.box6[L.gcell[L.grid[g].cell0].box6].first].chain};
         } else if (k == DK_BVH && leaf == item && dtree && dtreeLeaves(L, item)) {
             t = DTop{TOP_DTREE, i, 0, list_chain};  // (the leaves sit in the list's frame: no instance below)
         }
         L.top.push_back(t);
+    }
+    // grids are walked by MODE 8 only, the MODE 5 kernel with grid_walk: in
+    // worlds whose media (if any) are all TOP_MEDIUM items with sphere or Box
+    // boundaries; elsewhere the grid's tree is traversed as before
+    {
+        bool other = L.media_any;
+        std::vector<bool> topm(L.med.size(), false);
+        for (const DTop& t : L.top)
+            if (t.kind == TOP_MEDIUM) topm[t.a] = true;
+        for (size_t q = 0; q < topm.size(); q++) other = other || !topm[q];
+        L.grid_top = 0;
+        for (size_t q = 0; q < L.top.size(); q++) {
+            DTop& t = L.top[q];
+            if (t.kind != TOP_GRID) continue;
+            if (!other) {
+                L.grid_top++;
+                continue;
+            }
+            const uint32_t item = items[q];
+            t = dtree && dtreeLeaves(L, item) ? DTop{TOP_DTREE, item & INDEX_MASK, 0, list_chain}
+                                             : DTop{TOP_GENERIC, item, 0, list_chain};
+        }
     }
     // where the scan's ray changes (traverse_top): a new frame, and a new
     // direction when the frames' rotations (their RotateY sines and cosines,
@@ -4992,6 +5246,7 @@ int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32
     if (d.exact) return launchWaves<6, 16>(c, cam, P, bpc, st);
     if (d.simple && d.unit_time && d.n_wide && !c->dbg_out && !c->profile) return launchWide(c, cam, P, bpc, st);
     if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
+    if (d.n_grid) return launchStack<8>(c, cam, P, bpc, st);  // (buildTop keeps grids to MODE 2 / 5 worlds)
     if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
     if (!d.media_any && !d.media_nested) return launchStack<5>(c, cam, P, bpc, st);
     if (!d.media_any) return launchStack<4>(c, cam, P, bpc, st);
@@ -5303,6 +5558,10 @@ int rtow_scene_check(const rtow_scene* s, uint32_t* stack_need, uint32_t* chain_
         for (size_t j = 0; j < L.top.size(); j++)
             std::fprintf(stderr, "rtow-layout: top[%zu] kind %u flags %03x a %08x b %u chain %u\n", j,
                          L.top[j].kind & TOP_KIND_MASK, L.top[j].kind >> 8, L.top[j].a, L.top[j].b, L.top[j].chain);
+    if (std::getenv("RTOW_LAYOUT_INFO"))
+        for (const DGrid& g : L.grid)
+            std::fprintf(stderr, "rtow-layout: grid %ux%u axes %02x u %g..%g v %g..%g cell %g x %g h %g..%g margin %g (top %u)\n",
+                         g.nu, g.nv, g.axes, g.u0, g.u1, g.v0, g.v1, g.wu, g.wv, g.hlo, g.hhi, g.margin, L.grid_top);
     if (stack_need) *stack_need = L.stack_need;
     if (chain_need) *chain_need = L.chain_need;
     return RTOW_OK;
@@ -5372,6 +5631,10 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     size_t o_prog = pushBlob(blob, L.prog);
     if (L.box6.empty()) L.box6.push_back(DBox6{});
     size_t o_box6 = pushBlob(blob, L.box6);
+    const uint32_t n_grid = L.grid_top;
+    if (L.grid.empty()) L.grid.push_back(DGrid{});
+    if (L.gcell.empty()) L.gcell.push_back(DGridCell{});
+    size_t o_grid = pushBlob(blob, L.grid), o_gcell = pushBlob(blob, L.gcell);
     if (L.xh.empty()) L.xh.push_back(XHit{});
     if (L.xrefs.empty()) L.xrefs.push_back(0u);
     size_t o_xh = pushBlob(blob, L.xh), o_xrefs = pushBlob(blob, L.xrefs);
@@ -5415,6 +5678,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.rect_lmask = (const unsigned long long*)(b + o_lmask);
     d.prog = (const DProg*)(b + o_prog);
     d.box6 = (const DBox6*)(b + o_box6);
+    d.grid = (const DGrid*)(b + o_grid);
+    d.gcell = (const DGridCell*)(b + o_gcell);
+    d.n_grid = n_grid;
     for (int a = 0; a < 3; a++) d.tshift[a] = L.tshift[a];
     d.root = L.root;
     d.stack_need = L.stack_need;

@@ -203,6 +203,9 @@ struct alignas(16) DProg {  // 32 B; lo/hi read as ref_aabb_hit's (min xyz, -, m
 // (trace_dnodes) in the leaves' frame, entered once per ray; and so does a
 // BvhNode whose leaves are only spheres, rectangles and Boxes, with no
 // instance, list or medium below it (TOP_DTREE: final_ned's first tree).
+// A BvhNode whose leaves are Boxes tiling a regular grid of columns (final_ned's
+// 20 x 20 ground: equal cells along two axes, any extent along the third) is
+// walked as that grid (TOP_GRID, MODE 8): see DGrid.
 enum : uint32_t {
     TOP_GENERIC = 0,
     TOP_RECTS = 1,
@@ -210,7 +213,8 @@ enum : uint32_t {
     TOP_MEDIUM = 3,
     TOP_BOX6 = 4,
     TOP_SPHERES = 5,
-    TOP_DTREE = 6
+    TOP_DTREE = 6,
+    TOP_GRID = 7
 };
 // DTop::kind flags above the kind (buildTop): the item's frame differs from
 // the previous in-place item's (the scan recomputes its ray), and so does the
@@ -222,6 +226,31 @@ struct alignas(16) DTop {  // 16 B
     uint32_t a;      // GENERIC: item ref; RECTS: first rectangle; SPHERE: sphere; MEDIUM: medium
     uint32_t b;      // RECTS: count
     uint32_t chain;  // the chain of the leaf's frame (GENERIC: of the list's frame)
+};
+
+// TOP_GRID (a = grid index): Boxes whose extents along axes au and av are
+// exactly the cells [u0 + i wu, u0 + (i+1) wu] x [v0 + j wv, v0 + (j+1) wv] of an
+// nu x nv grid, one Box per cell, any extent [hlo, hhi] along the third axis ah
+// (a heightfield of columns).  Cell (i, j) is gcell[cell0 + j nu + i].  The
+// kernel walks the cells the ray crosses in order (rows along v, cells along u
+// within a row), every cell widened by `margin`, and scans the Box of every
+// cell the ray passes at a height the Box spans -- the same box6_scan the tree
+// runs, so the closest hit and its tie keys are the tree's.
+struct alignas(16) DGrid {  // 64 B
+    float u0, v0, wu, wv;
+    float iwu, iwv;   // 1 / wu, 1 / wv (rounded: cell indices are estimates, the margins cover them)
+    float hlo, hhi;   // the columns' extent along ah, over all cells
+    float u1, v1;     // the grid's far corner (every Box lies within [u0, u1] x [v0, v1])
+    uint32_t nu, nv;
+    uint32_t axes;    // au | av << 2 | ah << 4
+    uint32_t cell0;
+    float margin;     // spatial widening of every cell (and of the grid's box)
+    uint32_t pad;
+};
+struct alignas(16) DGridCell {  // 16 B
+    float hlo, hhi;  // the Box's extent along ah
+    uint32_t box6;   // its DBox6
+    uint32_t pad;
 };
 
 struct alignas(16) DMat {  // 32 B
@@ -255,6 +284,9 @@ struct DevScene {
     const DTop* top;         // general scenes: the top-level list, n_top items (0: none)
     const DProg* prog;       // programs of the BvhNode subtrees that hold media (DK_PROG)
     const DBox6* box6;       // Boxes among the rectangle lists (DList::box6, TOP_BOX6, MB_BOX6)
+    const DGrid* grid;       // TOP_GRID items (MODE 8)
+    const DGridCell* gcell;
+    uint32_t n_grid;
     uint32_t n_top;
     // Per rectangle: (offset << 8) | count of the boxes (8 floats each in
     // abox: min xyz, 0, max xyz, 0) of the reference BvhNodes above it in its

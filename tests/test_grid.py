@@ -1,0 +1,125 @@
+"""Boxes that tile a regular grid of columns, walked as a grid (TOP_GRID,
+MODE 8; rtow_device.hip grid_walk, DESIGN.md "Grids of Boxes").
+
+final_ned's ground -- BvhNode over 20 x 20 Boxes, 100 wide, 1..101 deep
+(scenes.h book-2 final scene; rtow_scene.cpp finalScene_NED) -- is detected at
+upload and scanned cell by cell along the ray instead of through its tree.
+The walk tests a superset of the Boxes any culled visit tests and scans each
+with the tree's own six-side test, so the frame must be bit-identical to the
+tree's (RTOW_GRID=0) and equal the oracle's, including rays that graze the
+columns (low cameras looking across the grid)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import rtow
+import scene_io as sio
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd")
+
+_LAYOUT = """
+import sys
+sys.path[:0] = [{pkg!r}, {tests!r}]
+import rtow, scene_io as sio
+sio.scene_check(rtow.Scene.build({scene!r}, n=100, image="synthetic"))
+"""
+
+
+def _layout(scene, **env):
+    code = _LAYOUT.format(pkg=PKG, tests=HERE, scene=scene)
+    e = dict(os.environ, RTOW_LAYOUT_INFO="1", **env)
+    r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return [ln for ln in r.stderr.splitlines() if ln.startswith("rtow-layout:")]
+
+
+def _top_kinds(lines):
+    return [int(ln.split(" kind ")[1].split()[0]) for ln in lines if " top[" in ln]
+
+
+TOP_GRID, TOP_DTREE = 7, 6
+
+
+def test_final_ned_ground_is_a_grid():
+    lines = _layout("final_ned")
+    grids = [ln for ln in lines if " grid " in ln]
+    assert len(grids) == 1 and "grid 20x20" in grids[0] and "cell 100 x 100" in grids[0] and "(top 1)" in grids[0]
+    kinds = _top_kinds(lines)
+    assert kinds.count(TOP_GRID) == 1
+    assert TOP_DTREE not in kinds  # the rest of the ground's run (light, four spheres) is scanned in place
+
+
+def test_grid_off_keeps_the_tree():
+    lines = _layout("final_ned", RTOW_GRID="0")
+    assert not [ln for ln in lines if " grid " in ln]
+    assert TOP_GRID not in _top_kinds(lines)
+
+
+@pytest.mark.parametrize("scene", ["cornell", "cornell_smoke", "random_ned"])
+def test_no_grid_elsewhere(scene):
+    lines = _layout(scene)
+    assert not [ln for ln in lines if " grid " in ln]
+
+
+def _low_camera(W, H, yaw_deg, pitch_deg, height):
+    """a camera just above final_ned's ground (world frame: the scene sits
+    under Translate(600, -278, 278); the columns reach from z = 278 up to
+    z = 177), looking across the grid"""
+    yaw, pitch = np.radians(yaw_deg), np.radians(pitch_deg)
+    cy, sy, cp, sp = np.cos(yaw), np.sin(yaw), np.cos(pitch), np.sin(pitch)
+    rows = [-cy * cp, -sy * cp, sp, -sy, cy, 0.0, -cy * sp, -sy * sp, -cp]
+    return rtow.camera_oriented(W, H, [600.0 + 150.0, -278.0 - 90.0, 278.0 - height], [float(v) for v in rows])
+
+
+CAMS = [("main", None), ("low_x", (0.0, 6.0, 120.0)), ("low_y", (90.0, -6.0, 110.0)),
+        ("low_diag", (45.0, 4.0, 104.0)), ("low_33", (33.0, -3.0, 140.0)), ("skim", (-60.0, 0.5, 102.0))]
+
+
+def _cam(W, H, spec):
+    return rtow.camera_main(W, H) if spec is None else _low_camera(W, H, *spec)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,spec", CAMS)
+def test_grid_frame_equals_tree_frame(name, spec, gpu_ctx):  # (gpu_ctx: torch's device first)
+    W, H, spp = 96, 72, 8
+    scene = rtow.Scene.build("final_ned", n=100, image="synthetic")
+    cam = _cam(W, H, spec)
+    p = rtow.params(W, H, spp, seed=11)
+    frames = []
+    for grid in ("1", "0"):
+        os.environ["RTOW_GRID"] = grid
+        try:
+            ctx = rtow.Context(0)
+            ctx.upload(scene)  # (the grid is chosen at upload)
+        finally:
+            os.environ.pop("RTOW_GRID", None)
+        _, lin, st = ctx.render(cam, p)
+        frames.append((lin.copy(), st.segments))
+        ctx.close()
+    (a, sa), (b, sb) = frames
+    print(f"GRID {name}: segments grid {sa} tree {sb}")
+    assert sa == sb
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,spec", CAMS[1:])
+def test_grid_matches_oracle_grazing(name, spec, gpu_ctx):
+    W, H, spp = 48, 36, 8
+    scene = rtow.Scene.build("final_ned", n=100, image="synthetic")
+    cam = _cam(W, H, spec)
+    p = rtow.params(W, H, spp, seed=23)
+    gpu_ctx.upload(scene)
+    _, lin, st = gpu_ctx.render(cam, p)
+    olin, _, oc = sio.oracle_render(scene.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p)))
+    a = np.asarray(lin, np.float64).reshape(-1, 3)
+    rms = np.sqrt(np.mean((a - olin.astype(np.float64)) ** 2, axis=0))
+    print(f"GRID-ORACLE {name}: rms {rms} segments gpu {st.segments} oracle {oc.segments}")
+    assert (rms <= 1e-4).all(), rms
+    assert st.segments == oc.segments
