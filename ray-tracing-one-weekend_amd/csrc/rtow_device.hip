@@ -713,6 +713,21 @@ __device__ __forceinline__ bool box6_nearest(const DevScene& S, uint32_t bi, con
     return f;
 }
 
+// Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
+struct Prof {
+    uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
+    uint32_t disc_pos, accepted, wave_mixed, wave_sph;  // sphere slots with disc > 0 / taken; waves running both slot paths / any sphere path
+    unsigned long long cyc_trav, cyc_other;  // wave cycles (s_memtime) in traversal / everything else
+    // general scenes: wave cycles per top-level item (first 8), in finalize, and the item visits
+    unsigned long long cyc_item[8], cyc_fin, visits_item[8], cyc_chain;
+    uint32_t box_lanes, box_waves;  // Box leaf scans in node steps: lanes / wave executions
+};
+
+__device__ __forceinline__ bool first_active_lane() {
+    const unsigned long long m = __ballot(1);
+    return (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1);
+}
+
 // TOP_GRID (MODE 8): the Boxes of a grid of columns (DGrid), walked along the
 // ray: rows along v in the ray's v order, within a row the cells along u in
 // its u order.  Every cell is widened by G.margin (2^-10 of a cell, hundreds
@@ -741,8 +756,9 @@ __device__ __forceinline__ void grid_band(float lo, float hi, float o, float id,
     t0 = flat ? (in ? -INFINITY : INFINITY) : n - fabsf(n) * REL;
     t1 = flat ? (in ? INFINITY : -INFINITY) : f + fabsf(f) * REL;
 }
+template <bool PROF = false>
 __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const Ray& r, const F3& inv, float tmin,
-                                          float& bt, uint32_t& best) {
+                                          float& bt, uint32_t& best, Prof* prof = nullptr) {
     constexpr float REL = 0x1p-18f;
     const DGrid G = cld(S.grid + gi);
     const uint32_t au = G.axes & 3u, av = (G.axes >> 2) & 3u, ah = (G.axes >> 4) & 3u;
@@ -762,12 +778,16 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
     const bool vflat = !(fabsf(iv) < INFINITY), uflat = !(fabsf(iu) < INFINITY);
     const int sv = dv < 0.0f ? -1 : 1, su = du < 0.0f ? -1 : 1;
     const float fnv = (float)(G.nv - 1u), fnu = (float)(G.nu - 1u);
-    auto row_of = [&](float t) {
+    // (the row of v, moved back / on by twice the widening: the rows whose
+    // widened bands hold the ray at te / tx; 1 / wv's rounding is 2^-23 of a
+    // cell per cell index, far inside the margin)
+    auto row_of = [&](float t, float back) {
         const float v = fmaf(t, dv, ov);
-        return fminf(fmaxf(floorf((v - G.v0) * G.iwv), -1.0f), (float)G.nv);
+        const float e = 2.0f * D + (fabsf(ov) + fabsf(v)) * REL;
+        return fminf(fmaxf(floorf((v + back * e - G.v0) * G.iwv), 0.0f), fnv);
     };
-    int j = (int)fminf(fmaxf(row_of(te) - (float)sv, 0.0f), fnv);
-    const int jl = (int)fminf(fmaxf(row_of(tx) + (float)sv, 0.0f), fnv);
+    int j = (int)row_of(te, -(float)sv);
+    const int jl = (int)row_of(tx, (float)sv);
     int nrows = (jl - j) * sv + 1;
     int i = 0, ncells = 0, jr = 0;
     float ra = 0.0f, rb = 0.0f;
@@ -775,6 +795,10 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
     while (live) {
         uint32_t cand = ~0u;
         while (true) {  // this lane's next cell to scan
+            if constexpr (PROF) {  // (instrumented kernel: walk steps, lanes / wave)
+                prof->lane_steps++;
+                if (first_active_lane()) prof->wave_steps++;
+            }
             const float bound = cull_bound(bt);
             if (ncells <= 0) {
                 if (nrows <= 0) {
@@ -794,12 +818,18 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
                 ra = fmaxf(t0, te);
                 rb = fminf(fminf(t1, tx), bound);
                 if (!(ra <= rb)) continue;
+                {  // the row's columns span [hlo, hhi] together (row record after the cells)
+                    const DGridCell R = S.gcell[G.cell0 + G.nu * G.nv + (uint32_t)jr];
+                    const float ha = fmaf(ra, dh, oh), hb = fmaf(rb, dh, oh);
+                    const float he = D + (fabsf(oh) + fmaxf(fabsf(ha), fabsf(hb))) * REL;
+                    if (fmaxf(ha, hb) + he < R.hlo || fminf(ha, hb) - he > R.hhi) continue;
+                }
                 // the row's cells: u over [ra, rb], widened
                 const float ua = fmaf(ra, du, ou), ub = fmaf(rb, du, ou);
                 const float ue = D + (fabsf(ou) + fmaxf(fabsf(ua), fabsf(ub))) * REL;
                 const float fa = floorf((fminf(ua, ub) - ue - G.u0) * G.iwu);
                 const float fb = floorf((fmaxf(ua, ub) + ue - G.u0) * G.iwu);
-                const int ia = (int)fminf(fmaxf(fa - 1.0f, 0.0f), fnu), ib = (int)fminf(fmaxf(fb + 1.0f, 0.0f), fnu);
+                const int ia = (int)fminf(fmaxf(fa, 0.0f), fnu), ib = (int)fminf(fmaxf(fb, 0.0f), fnu);
                 i = su > 0 ? ia : ib;
                 ncells = ib - ia + 1;
                 continue;
@@ -823,20 +853,17 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
             cand = C.box6;
             break;
         }
-        if (cand != ~0u && box6_scan(S, cand, r, inv, tmin, bt, best)) found = true;
+        if (cand != ~0u) {
+            if constexpr (PROF) {
+                prof->box_lanes++;
+                if (first_active_lane()) prof->box_waves++;
+            }
+            if (box6_scan(S, cand, r, inv, tmin, bt, best)) found = true;
+        }
     }
     return found;
 }
 
-// Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
-struct Prof {
-    uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
-    uint32_t disc_pos, accepted, wave_mixed, wave_sph;  // sphere slots with disc > 0 / taken; waves running both slot paths / any sphere path
-    unsigned long long cyc_trav, cyc_other;  // wave cycles (s_memtime) in traversal / everything else
-    // general scenes: wave cycles per top-level item (first 8), in finalize, and the item visits
-    unsigned long long cyc_item[8], cyc_fin, visits_item[8], cyc_chain;
-    uint32_t box_lanes, box_waves;  // Box leaf scans in node steps: lanes / wave executions
-};
 // General scenes: does leaf `cand`, hit at exactly the t of the current best
 // leaf `best`, take the record in the reference?  (assignTieKeys)
 __device__ __forceinline__ unsigned long long leaf_key(const DevScene& S, uint32_t ref) {
@@ -903,11 +930,6 @@ __device__ __forceinline__ bool tie_unsettled(const DevScene& S, uint32_t prim, 
         return false;
     }
     return false;  // the paths part at a BvhNode: both children see the same interval
-}
-
-__device__ __forceinline__ bool first_active_lane() {
-    const unsigned long long m = __ballot(1);
-    return (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1808,7 +1830,7 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         } else if (kind == TOP_DTREE) {
             trace_dnodes<STACK, true>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
         } else if (GRID && kind == TOP_GRID) {
-            grid_walk(S, T.a, r, inv, tmin, bt, bp);
+            grid_walk<PROF>(S, T.a, r, inv, tmin, bt, bp, prof);
         } else if (kind == TOP_SPHERE) {
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
@@ -3815,6 +3837,14 @@ struct GeneralSah {
             g.cell0 = (uint32_t)L.gcell.size();
             g.margin = (float)(std::max(wu, wv) * 0x1p-10);  // 2^2 x the tolerance above
             L.gcell.insert(L.gcell.end(), cells.begin(), cells.end());
+            for (uint32_t j = 0; j < nv; j++) {  // per row: the extent of its columns together
+                DGridCell row{FLT_MAX, -FLT_MAX, 0u, 0u};
+                for (uint32_t i = 0; i < nu; i++) {
+                    row.hlo = std::min(row.hlo, cells[(size_t)j * nu + i].hlo);
+                    row.hhi = std::max(row.hhi, cells[(size_t)j * nu + i].hhi);
+                }
+                L.gcell.push_back(row);
+            }
             L.grid_of[ref] = (uint32_t)L.grid.size();
             L.grid.push_back(g);
             return true;
@@ -3842,6 +3872,10 @@ struct GeneralSah {
             }
             uint32_t big = 0;
             for (const GenLeaf& g : run) big = std::max(big, leafCount(g.ref));
+            // (RTOW_RUNTREE=1: the rest of a run an aggregate was taken out of
+            // -- a grid, a sphere instance -- as a tree as well; A/B)
+            const char* rt = std::getenv("RTOW_RUNTREE");
+            if (rt && std::atoi(rt) != 0 && !alone.empty() && run.size() >= 2) big = 16;
             if (run.size() >= 2 && big >= 16) {
                 out.push_back(sahBuildBvh(run, 0, run.size(), L.bvh));
             } else {

@@ -231,7 +231,8 @@ struct alignas(16) DTop {  // 16 B
 // TOP_GRID (a = grid index): Boxes whose extents along axes au and av are
 // exactly the cells [u0 + i wu, u0 + (i+1) wu] x [v0 + j wv, v0 + (j+1) wv] of an
 // nu x nv grid, one Box per cell, any extent [hlo, hhi] along the third axis ah
-// (a heightfield of columns).  Cell (i, j) is gcell[cell0 + j nu + i].  The
+// (a heightfield of columns).  Cell (i, j) is gcell[cell0 + j nu + i], row j
+// (its columns together: hlo, hhi) gcell[cell0 + nu nv + j].  The
 // kernel walks the cells the ray crosses in order (rows along v, cells along u
 // within a row), every cell widened by `margin`, and scans the Box of every
 // cell the ray passes at a height the Box spans -- the same box6_scan the tree
