@@ -832,7 +832,7 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
                 const int ia = (int)fminf(fmaxf(fa, 0.0f), fnu), ib = (int)fminf(fmaxf(fb, 0.0f), fnu);
                 i = su > 0 ? ia : ib;
                 ncells = ib - ia + 1;
-                continue;
+                // (on to the row's first cell in the same step)
             }
             const int ic = i;
             i += su;
