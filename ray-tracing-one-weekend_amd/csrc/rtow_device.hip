@@ -756,6 +756,13 @@ __device__ __forceinline__ void grid_band(float lo, float hi, float o, float id,
     t0 = flat ? (in ? -INFINITY : INFINITY) : n - fabsf(n) * REL;
     t1 = flat ? (in ? INFINITY : -INFINITY) : f + fabsf(f) * REL;
 }
+// (the rows' and cells' bands: widened by the caller, see Eu, Ev)
+__device__ __forceinline__ void grid_band_w(float lo, float hi, float o, float id, bool flat, float& t0, float& t1) {
+    const float a = (lo - o) * id, b = (hi - o) * id;
+    const bool in = lo <= o && o <= hi;
+    t0 = flat ? (in ? -INFINITY : INFINITY) : fminf(a, b);
+    t1 = flat ? (in ? INFINITY : -INFINITY) : fmaxf(a, b);
+}
 template <bool PROF = false>
 __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const Ray& r, const F3& inv, float tmin,
                                           float& bt, uint32_t& best, Prof* prof = nullptr) {
@@ -786,6 +793,12 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
         const float e = 2.0f * D + (fabsf(ov) + fabsf(v)) * REL;
         return fminf(fmaxf(floorf((v + back * e - G.v0) * G.iwv), 0.0f), fnv);
     };
+    // the widening of every row and cell band and height test: the margin
+    // plus 2^-18 of the magnitudes the walk's coordinates reach within [te,
+    // tx] -- more than the rounding of o + t d, and of t = (x - o) (1 / d)
+    // carried back to a coordinate (|t d| 2^-22)
+    const float Eu = D + (fabsf(ou) + fabsf(tx * du)) * REL, Ev = D + (fabsf(ov) + fabsf(tx * dv)) * REL;
+    const float Eh = D + (fabsf(oh) + fabsf(tx * dh)) * REL;
     int j = (int)row_of(te, -(float)sv);
     const int jl = (int)row_of(tx, (float)sv);
     int nrows = (jl - j) * sv + 1;
@@ -807,7 +820,7 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
                 }
                 const float vlo = fmaf((float)j, G.wv, G.v0);
                 float t0, t1;
-                grid_band(vlo - D, vlo + G.wv + D, ov, iv, t0, t1);
+                grid_band_w(vlo - Ev, vlo + G.wv + Ev, ov, iv, vflat, t0, t1);
                 jr = j;
                 j += sv;
                 nrows--;
@@ -821,14 +834,12 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
                 {  // the row's columns span [hlo, hhi] together (row record after the cells)
                     const DGridCell R = S.gcell[G.cell0 + G.nu * G.nv + (uint32_t)jr];
                     const float ha = fmaf(ra, dh, oh), hb = fmaf(rb, dh, oh);
-                    const float he = D + (fabsf(oh) + fmaxf(fabsf(ha), fabsf(hb))) * REL;
-                    if (fmaxf(ha, hb) + he < R.hlo || fminf(ha, hb) - he > R.hhi) continue;
+                    if (fmaxf(ha, hb) + Eh < R.hlo || fminf(ha, hb) - Eh > R.hhi) continue;
                 }
                 // the row's cells: u over [ra, rb], widened
                 const float ua = fmaf(ra, du, ou), ub = fmaf(rb, du, ou);
-                const float ue = D + (fabsf(ou) + fmaxf(fabsf(ua), fabsf(ub))) * REL;
-                const float fa = floorf((fminf(ua, ub) - ue - G.u0) * G.iwu);
-                const float fb = floorf((fmaxf(ua, ub) + ue - G.u0) * G.iwu);
+                const float fa = floorf((fminf(ua, ub) - Eu - G.u0) * G.iwu);
+                const float fb = floorf((fmaxf(ua, ub) + Eu - G.u0) * G.iwu);
                 const int ia = (int)fminf(fmaxf(fa, 0.0f), fnu), ib = (int)fminf(fmaxf(fb, 0.0f), fnu);
                 i = su > 0 ? ia : ib;
                 ncells = ib - ia + 1;
@@ -839,7 +850,7 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
             ncells--;
             const float ulo = fmaf((float)ic, G.wu, G.u0);
             float c0, c1;
-            grid_band(ulo - D, ulo + G.wu + D, ou, iu, c0, c1);
+            grid_band_w(ulo - Eu, ulo + G.wu + Eu, ou, iu, uflat, c0, c1);
             c0 = fmaxf(c0, ra);
             c1 = fminf(fminf(c1, rb), bound);
             if (!(c0 <= c1)) {
@@ -848,8 +859,7 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
             }
             const DGridCell C = S.gcell[G.cell0 + (uint32_t)jr * G.nu + (uint32_t)ic];
             const float ha = fmaf(c0, dh, oh), hb = fmaf(c1, dh, oh);
-            const float he = D + (fabsf(oh) + fmaxf(fabsf(ha), fabsf(hb))) * REL;
-            if (fmaxf(ha, hb) + he < C.hlo || fminf(ha, hb) - he > C.hhi) continue;
+            if (fmaxf(ha, hb) + Eh < C.hlo || fminf(ha, hb) - Eh > C.hhi) continue;
             cand = C.box6;
             break;
         }
@@ -3872,10 +3882,11 @@ struct GeneralSah {
             }
             uint32_t big = 0;
             for (const GenLeaf& g : run) big = std::max(big, leafCount(g.ref));
-            // (RTOW_RUNTREE=1: the rest of a run an aggregate was taken out of
-            // -- a grid, a sphere instance -- as a tree as well; A/B)
+            // (RTOW_RUNTREE=k: the rest of a run an aggregate was taken out of
+            // -- a grid, a sphere instance -- as a tree as well when it holds
+            // >= k items; A/B)
             const char* rt = std::getenv("RTOW_RUNTREE");
-            if (rt && std::atoi(rt) != 0 && !alone.empty() && run.size() >= 2) big = 16;
+            if (rt && std::atoi(rt) != 0 && !alone.empty() && run.size() >= (size_t)std::max(2, std::atoi(rt))) big = 16;
             if (run.size() >= 2 && big >= 16) {
                 out.push_back(sahBuildBvh(run, 0, run.size(), L.bvh));
             } else {

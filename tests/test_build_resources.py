@@ -31,8 +31,8 @@ LIB = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "librtow_hip.so")
 # variants: 12 / 8 B since trace_dnodes tests leaf slots in place, TOP_DTREE --
 # cornell unchanged, A/B; the config-5 kernel, MODE 5 at STACK 16, has none:
 # test_config5_kernel_has_no_scratch)
-SCRATCH_BOUND = {0: 0, 2: 12, 4: 24, 3: 96, 5: 8, 6: 0, 7: 24, 8: 12}  # 7: the 4-wide tree (RTOW_WIDE, experiment)
-# (8: MODE 5 with the grid walk, TOP_GRID: config 5's kernel since round 4, 8 B at STACK 16)
+SCRATCH_BOUND = {0: 0, 2: 12, 4: 24, 3: 96, 5: 8, 6: 0, 7: 24, 8: 24}  # 7: the 4-wide tree (RTOW_WIDE, experiment)
+# (8: MODE 5 with the grid walk, TOP_GRID: config 5's kernel since round 4, 12 B at STACK 16, 24 B at 20 and 32)
 
 
 @pytest.fixture(scope="module")
@@ -56,11 +56,17 @@ def test_bench_kernel_has_no_scratch(kernels):
     assert hot[0]["vgpr"] <= 128  # 4 waves per SIMD
 
 
-def test_config5_kernel_has_no_scratch(kernels):
-    k5 = [k for k in kernels if codeobj.demangled_params(k["name"]) ==
-          {"MODE": 5, "STACK": 16, "WAVES": 4, "PROF": 0, "BS": 256, "LDSN": 0, "DBG": 0}]
-    assert len(k5) == 1
-    assert k5[0]["scratch"] == 0 and k5[0]["vgpr_spill"] == 0
+def test_general_config_kernels_scratch(kernels):
+    """configs 3 and 4 run MODE 5 at STACK 16 (no scratch); config 5 runs
+    MODE 8, the same kernel with the grid walk (final_ned's ground), 12 B"""
+    def one(mode):
+        ks = [k for k in kernels if codeobj.demangled_params(k["name"]) ==
+              {"MODE": mode, "STACK": 16, "WAVES": 4, "PROF": 0, "BS": 256, "LDSN": 0, "DBG": 0}]
+        assert len(ks) == 1
+        return ks[0]
+    k5, k8 = one(5), one(8)
+    assert k5["scratch"] == 0 and k5["vgpr_spill"] == 0
+    assert k8["scratch"] <= 12 and k8["vgpr"] <= 128
 
 
 def test_default_kernels_scratch_bounded(kernels):
