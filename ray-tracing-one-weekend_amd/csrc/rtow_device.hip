@@ -793,12 +793,16 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
         const float e = 2.0f * D + (fabsf(ov) + fabsf(v)) * REL;
         return fminf(fmaxf(floorf((v + back * e - G.v0) * G.iwv), 0.0f), fnv);
     };
-    // the widening of every row and cell band and height test: the margin
-    // plus 2^-18 of the magnitudes the walk's coordinates reach within [te,
-    // tx] -- more than the rounding of o + t d, and of t = (x - o) (1 / d)
-    // carried back to a coordinate (|t d| 2^-22)
+    // the widening of every row and cell band: the margin plus 2^-18 of the
+    // magnitudes the walk's coordinates reach within [te, tx] -- more than
+    // the rounding of o + t d, and of t = (x - o) (1 / d) carried back to a
+    // coordinate (|t d| 2^-22).  The height tests need no margin: a Box spans
+    // exactly its cell's [hlo, hhi], so only roundings separate a hit's
+    // height from that range -- the face test's point (2 roundings of o + t d)
+    // and ha / hb here (one), far below 2^-18 of the magnitudes.  (A margin
+    // there would make every ray leaving a column's top scan that column.)
     const float Eu = D + (fabsf(ou) + fabsf(tx * du)) * REL, Ev = D + (fabsf(ov) + fabsf(tx * dv)) * REL;
-    const float Eh = D + (fabsf(oh) + fabsf(tx * dh)) * REL;
+    const float Eh = (fabsf(oh) + fabsf(tx * dh)) * REL;
     int j = (int)row_of(te, -(float)sv);
     const int jl = (int)row_of(tx, (float)sv);
     int nrows = (jl - j) * sv + 1;
