@@ -123,3 +123,80 @@ def test_grid_matches_oracle_grazing(name, spec, gpu_ctx):
     print(f"GRID-ORACLE {name}: rms {rms} segments gpu {st.segments} oracle {oc.segments}")
     assert (rms <= 1e-4).all(), rms
     assert st.segments == oc.segments
+
+
+def _flat_topped(levels=(-30.0, -60.0)):
+    """final_ned with every ground Box cut to one of a few heights (box.h: the
+    sides' planes and extents follow pMin.z), BVH boxes refreshed: neighbouring
+    columns share their top planes and side planes, so rays meet exact ties
+    between Boxes -- settled by the tie keys, whichever order the walk or the
+    tree scans them"""
+    d = sio.scene_dict(rtow.Scene.build("final_ned", n=100, image="synthetic"))
+    h = d["hitables"]
+    HIT_BOX, HIT_FLIP = 10, 6
+    boxes = [i for i in range(len(h)) if h[i]["kind"] == HIT_BOX]
+    assert len(boxes) == 400
+    for q, b in enumerate(boxes):
+        z = np.float32(levels[(q * 7 + q // 20) % len(levels)])  # the NED box spans z in [-y1, 0]
+        h[b]["f"][2] = z
+        first = int(h[int(h[b]["a"])]["a"])
+        sides = [int(r) for r in d["refs"][first:first + 6]]
+        rect = [s if h[s]["kind"] != HIT_FLIP else int(h[s]["a"]) for s in sides]
+        h[rect[1]]["f"][4] = z  # XY at z0
+        for k in (2, 3, 4, 5):  # XZ and YZ sides: their z range [z0, z1] in f[2]
+            h[rect[k]]["f"][2] = z
+
+    def box(i):
+        e = h[i]
+        if e["kind"] == HIT_BOX:
+            return e["f"][:3].copy(), e["f"][3:6].copy()
+        if e["kind"] == sio.HIT_BVH_NODE:
+            a0, a1 = box(int(e["a"]))
+            b0, b1 = box(int(e["b"]))
+            lo, hi = np.minimum(a0, b0), np.maximum(a1, b1)
+            e["f"][:3], e["f"][3:6] = lo, hi
+            return lo, hi
+        raise ValueError(int(e["kind"]))
+
+    r = int(d["root"])
+    while int(h[r]["kind"]) == sio.HIT_TRANSLATE:
+        r = int(h[r]["a"])
+    ground = int(d["refs"][int(h[r]["a"])])  # the world list's first item: BvhNode over the 400 Boxes
+    assert h[ground]["kind"] == sio.HIT_BVH_NODE
+    box(ground)
+    return d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,spec", [CAMS[0], CAMS[1], CAMS[3]])
+def test_flat_topped_grid_ties(name, spec, gpu_ctx):
+    W, H, spp = 48, 36, 8
+    arr = sio.ArrayScene(_flat_topped())
+    cam = _cam(W, H, spec)
+    p = rtow.params(W, H, spp, seed=31)
+    frames = []
+    for grid in ("1", "0"):
+        os.environ["RTOW_GRID"] = grid
+        try:
+            ctx = rtow.Context(0)
+            ctx.upload(arr)
+        finally:
+            os.environ.pop("RTOW_GRID", None)
+        _, lin, st = ctx.render(cam, p)
+        frames.append((lin.copy(), st.segments))
+        ctx.close()
+    (a, sa), (b, sb) = frames
+    assert sa == sb and np.array_equal(a, b)
+    olin, _, oc = sio.oracle_render(arr.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p)))
+    x = np.asarray(a, np.float64).reshape(-1, 3)
+    rms = np.sqrt(np.mean((x - olin.astype(np.float64)) ** 2, axis=0))
+    print(f"GRID-FLAT {name}: rms {rms} segments gpu {sa} oracle {oc.segments}")
+    assert (rms <= 1e-4).all(), rms
+    assert sa == oc.segments
+
+
+def test_flat_topped_world_is_a_grid():
+    """the edited world still passes the upload checks and keeps its grid"""
+    arr = sio.ArrayScene(_flat_topped())
+    assert rtow.lib().rtow_scene_check(arr.view_ptr, None, None) == rtow.OK
