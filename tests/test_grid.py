@@ -200,3 +200,80 @@ def test_flat_topped_world_is_a_grid():
     """the edited world still passes the upload checks and keeps its grid"""
     arr = sio.ArrayScene(_flat_topped())
     assert rtow.lib().rtow_scene_check(arr.view_ptr, None, None) == rtow.OK
+
+
+def _shift_one_box(dx=1.0, which=137):
+    """final_ned with one ground Box moved dx along x (its six sides with it,
+    BVH boxes refreshed): it no longer sits in its cell"""
+    d = sio.scene_dict(rtow.Scene.build("final_ned", n=100, image="synthetic"))
+    h = d["hitables"]
+    HIT_BOX, HIT_FLIP = 10, 6
+    b = [i for i in range(len(h)) if h[i]["kind"] == HIT_BOX][which]
+    first = int(h[int(h[b]["a"])]["a"])
+    sides = [int(r) for r in d["refs"][first:first + 6]]
+    rect = [s if h[s]["kind"] != HIT_FLIP else int(h[s]["a"]) for s in sides]
+    dx = np.float32(dx)
+    for k in (0, 1, 2, 3):  # XY and XZ sides: x range in f[0], f[1]
+        h[rect[k]]["f"][0] += dx
+        h[rect[k]]["f"][1] += dx
+    for k in (4, 5):  # YZ sides: their plane x = k
+        h[rect[k]]["f"][4] += dx
+    h[b]["f"][0] += dx
+    h[b]["f"][3] += dx
+
+    def box(i):
+        e = h[i]
+        if e["kind"] == HIT_BOX:
+            return e["f"][:3].copy(), e["f"][3:6].copy()
+        a0, a1 = box(int(e["a"]))
+        b0, b1 = box(int(e["b"]))
+        lo, hi = np.minimum(a0, b0), np.maximum(a1, b1)
+        e["f"][:3], e["f"][3:6] = lo, hi
+        return lo, hi
+
+    r = int(d["root"])
+    while int(h[r]["kind"]) == sio.HIT_TRANSLATE:
+        r = int(h[r]["a"])
+    box(int(d["refs"][int(h[r]["a"])]))
+    return d
+
+
+@pytest.mark.parametrize("dx,grid", [(1.0, False), (0.01, True)])
+def test_grid_detection_tolerance(dx, grid, capfd, monkeypatch):
+    """a Box more than 2^-12 of a cell off its cell (1 unit of 100) leaves the
+    ground a tree; 0.01 units (inside the tolerance, far inside the walk's
+    2^-10 margin) keeps the grid"""
+    monkeypatch.setenv("RTOW_LAYOUT_INFO", "1")
+    arr = sio.ArrayScene(_shift_one_box(dx))
+    assert rtow.lib().rtow_scene_check(arr.view_ptr, None, None) == rtow.OK
+    err = capfd.readouterr().err
+    assert ("rtow-layout: grid 20x20" in err) == grid
+
+
+@pytest.mark.gpu
+def test_grid_with_a_box_off_its_cell(gpu_ctx):
+    """a Box 0.01 units off its cell (inside the detection tolerance): the walk's
+    margin still reaches it -- grid and tree frames identical, oracle parity"""
+    W, H, spp = 48, 36, 8
+    arr = sio.ArrayScene(_shift_one_box(0.01))
+    cam = _cam(W, H, CAMS[1][1])
+    p = rtow.params(W, H, spp, seed=37)
+    frames = []
+    for grid in ("1", "0"):
+        os.environ["RTOW_GRID"] = grid
+        try:
+            ctx = rtow.Context(0)
+            ctx.upload(arr)
+        finally:
+            os.environ.pop("RTOW_GRID", None)
+        _, lin, st = ctx.render(cam, p)
+        frames.append((lin.copy(), st.segments))
+        ctx.close()
+    (a, sa), (b, sb) = frames
+    assert sa == sb and np.array_equal(a, b)
+    olin, _, oc = sio.oracle_render(arr.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p)))
+    x = np.asarray(a, np.float64).reshape(-1, 3)
+    rms = np.sqrt(np.mean((x - olin.astype(np.float64)) ** 2, axis=0))
+    assert (rms <= 1e-4).all(), rms
+    assert sa == oc.segments
