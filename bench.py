@@ -97,6 +97,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-kind", choices=["auto", "port"], default="auto",
                     help="auto: the reference's own code when oracle/_ref was built, else the oracle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every host CPU this process may use")
+    ap.add_argument("--inproc", action="store_true",
+                    help="one process drives all --gpus N devices through the C-ABI's own multi-GPU render "
+                         "(rtow_multi_render: a host thread per device, one RCCL gather, assembly on device 0; "
+                         "every rank chunks as the whole frame), instead of one process per GPU")
     ap.add_argument("--pmc-json", default=None,
                     help="PMC summary to use (default: the newest profiles/*/pmc_summary.json of this build+config)")
     args = ap.parse_args(argv)
@@ -388,6 +392,51 @@ class HipRank:
         self.ctx.close()
 
 
+class InprocRank(HipRank):
+    """--inproc: the C-ABI's multi-GPU render in this one process --
+    rtow_multi_render over devices 0..N-1 (rtow_multi.cpp: one rtow_context and
+    stream per device, all rendering at once from their own host threads, one
+    RCCL gather of the tile slabs to device 0, the BGRA frame assembled there
+    and left on the device, as the default path leaves it).  What main.cpp's
+    binding would call; no torch.distributed."""
+
+    backend = None
+
+    def __init__(self, args, rank, world, local):
+        import torch
+
+        import rtow
+
+        assert world == 1 and rank == 0, "--inproc runs as one process"
+        self.args, self.rank = args, 0
+        self.world = self.n_gpus = args.gpus
+        torch.cuda.set_device(0)
+        self.device = torch.device("cuda", 0)
+        W, H = args.width, args.height
+        self.scene = rtow.Scene.build(args.scene, n=max(args.n, 1), image="synthetic", scene_seed=1)
+        self.cam = rtow.camera_main(W, H)
+        self.multi = rtow.Multi(list(range(self.n_gpus)))
+        self.multi.upload(self.scene)
+        self.p = rtow.params(W, H, args.spp, seed=args.seed)
+        self.device_kms = []
+        if not args.no_prime:
+            self.multi.render(self.cam, rtow.params(W, H, 1, seed=args.seed), linear=False, host=False)
+
+    def step(self, dist):
+        _, _, st, dst = self.multi.render(self.cam, self.p, linear=False, host=False)
+        self.device_kms.append([d.kernel_ms for d in dst])
+        return st
+
+    def report(self, segs, steps, mean_kms):
+        # the roofline prices one device's kernel: its share of the rays (the
+        # 8x8-tile interleave balances the shares within ~0.5 %) over the
+        # slowest device's kernel time
+        return super().report(segs / self.n_gpus, steps, mean_kms)
+
+    def close(self):
+        self.multi.close()
+
+
 def run(args, make_rank):
     """The timed loop of every rank: W warmup steps, then exactly K steps
     between barrier + device synchronize on both sides; the whole-job rate is
@@ -400,6 +449,7 @@ def run(args, make_rank):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     R = make_rank(args, rank, world, local)
     distributed = world > 1
+    n_gpus = getattr(R, "n_gpus", world)  # --inproc: one process, N devices
     if distributed:
         dist.init_process_group(R.backend, **R.init_kwargs())
 
@@ -432,6 +482,8 @@ def run(args, make_rank):
         dist.all_gather(rank_kms, rk)
     segs_all, samples_all, elapsed = float(tot[0]), float(tot[1]), float(el[0])
     per_rank = [round(float(t[0]), 2) for t in rank_kms]
+    if getattr(R, "device_kms", None):  # --inproc: every device's mean kernel time
+        per_rank = [round(float(x), 2) for x in np.mean(np.asarray(R.device_kms), axis=0)]
 
     if rank == 0:
         scene, _, W0, H0, spp0, label = WORKLOADS[args.workload]
@@ -444,7 +496,7 @@ def run(args, make_rank):
             "value": round(segs_all / elapsed / 1e6, 2),
             "unit": "Mray/s",
             "msample_per_s": round(samples_all / elapsed / 1e6, 3),
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / max(args.steps, 1), 2),
@@ -458,7 +510,9 @@ def run(args, make_rank):
                                    + f"{W}x{H}x{spp}spp, depth 50, synthetic 2048x1024 earth texture",
                        "scene": scene, "width": W, "height": H, "spp": spp, "n": args.n, "scene_seed": 1,
                        "render_seed": args.seed, "baseline_config": is_baseline_cfg,
-                       "parallelism": f"tiles8x8 interleaved over {world} rank(s) + gather to rank 0"},
+                       "parallelism": (f"tiles8x8 interleaved over {n_gpus} device(s) of one process "
+                                       "(rtow_multi_render: RCCL gather to device 0)" if args.inproc else
+                                       f"tiles8x8 interleaved over {world} rank(s) + gather to rank 0")},
             "rays_per_sample": round(segs_all / max(samples_all, 1), 4),
             "rays_per_step": int(segs_all / max(args.steps, 1)),
             "rank_kernel_ms": {"min": min(per_rank), "max": max(per_rank), "per_rank": per_rank},
@@ -473,6 +527,12 @@ def run(args, make_rank):
 def main(make_rank=HipRank, argv=None):
     args = parse(argv)
     world_env = os.environ.get("WORLD_SIZE")
+    if args.inproc:
+        if world_env not in (None, "1"):
+            print("bench.py: --inproc is one process; do not launch it with torch.distributed", file=sys.stderr)
+            sys.exit(2)
+        run(args, InprocRank if make_rank is HipRank else make_rank)
+        return
     if world_env is None and args.gpus > 1:
         # N ranks were asked for and none were launched: start them (one
         # process per GPU) instead of running one rank and reporting it

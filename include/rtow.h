@@ -176,10 +176,18 @@ typedef struct rtow_camera {
  * rank r of `world` renders tiles r, r+world, r+2*world, ... (the reference's
  * column interleave main.cpp:936, done by tiles). */
 enum {
-    RTOW_FLAG_STATS = 1u << 0,     /* count segments (color() calls) on device */
-    RTOW_FLAG_CAMERA_DOF = 1u << 1 /* CAMERA_DOF_EN 1 (defines.h:26; off in the reference's
-                                      build): Camera::getRay's offset is _lensRadius *
-                                      randomInUnitDisk() + randomInUnitSphere() (camera.h:124-126) */
+    RTOW_FLAG_STATS = 1u << 0,      /* count segments (color() calls) on device */
+    RTOW_FLAG_CAMERA_DOF = 1u << 1, /* CAMERA_DOF_EN 1 (defines.h:26; off in the reference's
+                                       build): Camera::getRay's offset is _lensRadius *
+                                       randomInUnitDisk() + randomInUnitSphere() (camera.h:124-126) */
+    RTOW_FLAG_FRAME_PLAN = 1u << 2  /* automatic chunking (samples_per_chunk 0) plans for the whole
+                                       frame -- as rank 0 of world 1 -- whatever p->rank / p->world:
+                                       every rank cuts its pixels' samples into the chunks rtow_render
+                                       cuts, so the chunks' float sums, and the assembled frame, equal
+                                       rtow_render's bit for bit.  Without it a rank's share plans for
+                                       its own pixel count (shorter chunks on more ranks: a shorter
+                                       grid tail, but other float chunk sums, so the last bits of the
+                                       frame depend on the world size).  rtow_multi_render sets it. */
 };
 
 typedef struct rtow_params {
@@ -198,7 +206,10 @@ typedef struct rtow_params {
     uint64_t seed;              /* render stream seed (rtow_rng.h) */
     uint32_t rank, world;       /* tile partition; world 0 is treated as 1 */
     uint32_t flags;
-    uint32_t blocks_per_cu;     /* persistent-grid occupancy; 0 = auto */
+    uint32_t blocks_per_cu;     /* persistent-grid blocks per CU; 0 = auto (the kernel's occupancy).
+                                    Capped at that occupancy: blocks that cannot be resident add
+                                    nothing to a persistent grid, so a larger request silently gets
+                                    the occupancy (no error) */
 } rtow_params;
 
 typedef struct rtow_stats {

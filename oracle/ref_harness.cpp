@@ -418,6 +418,7 @@ struct Opts {
     uint64_t seed = 1;
     int threads = 0;
     bool racy = false;
+    int ranks = 0;  // dropin_multi: ranks over device 0 (0: every visible device once)
     std::string cwd;
 };
 
@@ -583,6 +584,7 @@ static Opts parseOpts(int argc, char** argv, int first) {
         else if (a == "--threads") o.threads = std::atoi(next());
         else if (a == "--cwd") o.cwd = next();
         else if (a == "--racy") o.racy = true;
+        else if (a == "--ranks") o.ranks = std::atoi(next());
         else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); std::exit(2); }
     }
     return o;
@@ -742,6 +744,65 @@ int main(int argc, char** argv) {
         std::fclose(f);
         std::printf("{\"segments\": %llu, \"samples\": %llu, \"kernel_ms\": %.3f}\n",
                     (unsigned long long)st.segments, (unsigned long long)st.samples, st.kernel_ms);
+        return 0;
+    }
+    if (cmd == "dropin_multi" && argc >= 7) {
+        // The multi-GPU binding of INTEGRATION.md, in the reference's own TU:
+        // every visible device renders its share of the frame main.cpp's N
+        // worker threads would have split by columns (main.cpp:182-195, 936),
+        // one RCCL gather, the frame assembled on device 0 (rtow_render_devices).
+        // --ranks k instead lists device 0 k times (ranks sharing one device,
+        // gathered by device copies).  Prints which librccl the process loaded.
+        Opts o = parseOpts(argc, argv, 7);
+        uint32_t W = (uint32_t)std::atoi(argv[3]), H = (uint32_t)std::atoi(argv[4]);
+        uint32_t spp = (uint32_t)std::atoi(argv[5]);
+        std::string prefix = argv[6];
+        Hitable* world = buildWorld(argv[2], o);
+        Camera* cam = mainCamera(W, H);
+        rtow_ref::World w(world);
+        rtow_camera rc;
+        if (w.status() != RTOW_OK || rtow_ref::camera(*cam, &rc) != RTOW_OK) return 3;
+        int count = 0;
+        if (rtow_device_count(&count) != RTOW_OK || count < 1) {
+            std::fprintf(stderr, "dropin_multi: no device (%s)\n", rtow_last_error());
+            return 4;
+        }
+        std::vector<int> devices;
+        if (o.ranks > 0) devices.assign((size_t)o.ranks, 0);
+        else for (int d = 0; d < count; d++) devices.push_back(d);
+        rtow_params p;
+        rtow_ref::params(W, H, spp, &p);
+        p.seed = o.seed;
+        std::vector<uint8_t> bgra((size_t)W * H * 4);
+        std::vector<float> lin((size_t)W * H * 3);
+        rtow_stats st{};
+        int rc2 = rtow_render_devices(devices.data(), (uint32_t)devices.size(), w.view(), &rc, &p, bgra.data(),
+                                      lin.data(), &st);
+        if (rc2 != RTOW_OK) {
+            std::fprintf(stderr, "dropin_multi: %s (%s)\n", rtow_error_string(rc2), rtow_last_error());
+            return 4;
+        }
+        std::string rccl = "none";
+        if (FILE* maps = std::fopen("/proc/self/maps", "r")) {
+            char line[4096];
+            while (std::fgets(line, sizeof line, maps))
+                if (const char* q = std::strstr(line, "/librccl.so")) {
+                    const char* b = std::strchr(line, '/');
+                    rccl.assign(b, q + std::strlen("/librccl.so") - b);
+                    break;
+                }
+            std::fclose(maps);
+        }
+        FILE* f = std::fopen((prefix + ".lin").c_str(), "wb");
+        std::fwrite(lin.data(), 4, lin.size(), f);
+        std::fclose(f);
+        f = std::fopen((prefix + ".bgra").c_str(), "wb");
+        std::fwrite(bgra.data(), 1, bgra.size(), f);
+        std::fclose(f);
+        std::printf("{\"segments\": %llu, \"samples\": %llu, \"kernel_ms\": %.3f, \"total_ms\": %.3f, "
+                    "\"ranks\": %zu, \"devices_visible\": %d, \"librccl\": \"%s\"}\n",
+                    (unsigned long long)st.segments, (unsigned long long)st.samples, st.kernel_ms, st.total_ms,
+                    devices.size(), count, rccl.c_str());
         return 0;
     }
 #endif

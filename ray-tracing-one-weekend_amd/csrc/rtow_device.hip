@@ -82,6 +82,12 @@ __device__ __forceinline__ F3 unit(F3 v) {
 }
 __device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]); }
 
+// make EXPERIMENTS=1: also build the measured-slower 4-wide tree (MODE 7,
+// RTOW_WIDE / RTOW_SPEC); the default library leaves it out
+#ifndef RTOW_EXPERIMENTS
+#define RTOW_EXPERIMENTS 0
+#endif
+
 // Scene records read through the constant address space: the scene is
 // read-only for a kernel's lifetime, and a load whose address is uniform
 // across the wave (the top-level scan's items, their instance chains, Box
@@ -3056,7 +3062,9 @@ RTOW_KLIST_G(RTOW_KX, 3)
 RTOW_KLIST_G(RTOW_KX, 4)
 RTOW_KLIST_G(RTOW_KX, 5)
 RTOW_KLIST_6(RTOW_KX)
+#if RTOW_EXPERIMENTS
 RTOW_KLIST_7(RTOW_KX)
+#endif
 RTOW_KLIST_8(RTOW_KX)
 #endif
 #undef RTOW_KX
@@ -5279,8 +5287,9 @@ int launchStack(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t
     return set_error(RTOW_E_UNSUPPORTED, "scene needs a traversal stack deeper than 64 entries");
 }
 
+#if RTOW_EXPERIMENTS
 // MODE 7: the simple scene over its 4-wide tree (RTOW_WIDE), 512-thread
-// blocks with the tree in LDS, the only variants built (hot kernel TU)
+// blocks with the tree in LDS, the only variants built (make EXPERIMENTS=1)
 int launchWide(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const uint32_t need = c->scene.wide_need + 1;  // (+ the sentinel entry; 16-bit entries, two per stack word)
     if (need <= 32 && lds_bytes(16, 512, 2 * c->scene.n_wide, true) <= 80 * 1024)
@@ -5289,11 +5298,14 @@ int launchWide(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t 
         return launchTrace<7, 32, 4, false, 512, true>(c, cam, P, bpc, st);
     return launchStack<0>(c, cam, P, bpc, st);  // too large for LDS: the binary tree (same frame)
 }
+#endif
 
 int dispatchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const DevScene& d = c->scene;
     if (d.exact) return launchWaves<6, 16>(c, cam, P, bpc, st);
+#if RTOW_EXPERIMENTS
     if (d.simple && d.unit_time && d.n_wide && !c->dbg_out && !c->profile) return launchWide(c, cam, P, bpc, st);
+#endif
     if (d.simple && d.unit_time) return launchStack<0>(c, cam, P, bpc, st);
     if (d.n_grid) return launchStack<8>(c, cam, P, bpc, st);  // (buildTop keeps grids to MODE 2 / 5 worlds)
     if (!d.has_media) return launchStack<2>(c, cam, P, bpc, st);
@@ -5323,8 +5335,12 @@ int planParams(int cus, uint32_t auto_spc, const rtow_params* p, DevParams& P) {
     // 32-sample 146.4, 16-sample 149.0 -- round 2's bound of 60 items per lane
     // picked 16; 30 picks 32.  Config 2 gets 128 on one or two GPUs, 64 on
     // four, 32 on eight; config 5's shares get 128.
-    // RTOW_AUTO_SPC (c->auto_spc) fixes the length instead.
-    const uint32_t n_px = rtow_rank_tile_count(p->width, p->height, p->rank, world) * 64u;
+    // RTOW_AUTO_SPC (c->auto_spc) fixes the length instead.  RTOW_FLAG_FRAME_PLAN
+    // plans every rank's share as the whole frame (rank 0 of world 1), so its
+    // chunks -- and their float sums -- are rtow_render's.
+    const bool frame_plan = (p->flags & RTOW_FLAG_FRAME_PLAN) != 0;
+    const uint32_t n_px = rtow_rank_tile_count(p->width, p->height, frame_plan ? 0u : p->rank,
+                                               frame_plan ? 1u : world) * 64u;
     uint32_t spc = p->samples_per_chunk;
     if (!spc && auto_spc) spc = auto_spc;
     if (!spc) {
@@ -5539,7 +5555,9 @@ int rtow_context_create(int device, rtow_context** out) {
     if (const char* ln = std::getenv("RTOW_LDS_NODES")) c->lds_nodes = std::atoi(ln);
     if (const char* sc = std::getenv("RTOW_AUTO_SPC")) c->auto_spc = std::max(1, std::atoi(sc));
     if (const char* tr = std::getenv("RTOW_BVH")) c->tree = std::string(tr) == "ref" ? RTOW_TREE_REFERENCE : RTOW_TREE_SAH;
+#if RTOW_EXPERIMENTS  // (the MODE 7 kernels exist only in an EXPERIMENTS=1 build)
     if (const char* wd = std::getenv("RTOW_WIDE")) c->wide = (uint32_t)std::max(0, std::atoi(wd));
+#endif
     if (const char* sv = std::getenv("RTOW_SPEC")) c->spec = (uint32_t)std::max(0, std::atoi(sv));
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail(set_error(RTOW_E_HIP, hipGetErrorString(e)));

@@ -2,24 +2,36 @@
 //
 // The reference renders one frame with N std::threads over a shared buffer,
 // thread i taking columns i, i+N, ... (main.cpp:182-195 start them, main.cpp:936
-// interleaves the columns).  Here device i of n is rank i of world n: it renders
-// the 8x8 tiles i, i+n, ... of the frame into a compact slab on its own stream
-// (rtow_render_tiles_device), all devices at once (one host thread each: a
-// render call returns when its device is done), then ONE RCCL gather brings
-// the slabs to device 0 over xGMI -- communicators from ncclCommInitAll, the
-// gather as grouped ncclSend / ncclRecv (RCCL has no gather primitive) -- and
-// device 0 assembles the frame (rtow_assemble_device / _linear_device).
+// interleaves the columns).  Here entry i of the device list is rank i of world
+// n: it renders the 8x8 tiles i, i+n, ... of the frame into a compact slab on
+// its own stream (rtow_render_tiles_device), all ranks at once (one host thread
+// each: a render call returns when its work is done), then ONE gather brings
+// the slabs to the first device and that device assembles the frame
+// (rtow_assemble_device / _linear_device):
+//   - n distinct devices: RCCL over xGMI -- communicators from ncclCommInitAll,
+//     the gather as grouped ncclSend / ncclRecv (RCCL has no gather primitive);
+//   - a device listed more than once (its ranks share it: each its own context
+//     and stream; RCCL allows one rank per device): device copies
+//     (hipMemcpyPeerAsync) onto the first device's stream.
+// Every rank plans its chunks as the whole frame (RTOW_FLAG_FRAME_PLAN), so the
+// frame equals rtow_render's bit for bit for any n.
+//
+// RCCL is opened on the first rtow_multi_create that needs it (dlopen of
+// librccl.so.1, then $(ROCM)/lib's), so a caller that never uses several GPUs
+// loads librtow_hip.so without it; missing RCCL is RTOW_E_RCCL.
 //
 // Host code over the public C-ABI plus HIP streams and RCCL; the kernels are
 // rtow_device.hip's.  Payload: config 2's BGRA frame is 8.3 MB (1 MB per rank
 // at n = 8), config 5's 67 MB -- microseconds to milliseconds against seconds
 // of rendering.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -27,14 +39,19 @@
 #include "../../include/rtow.h"
 #include "rtow_internal.h"
 
+#ifndef RTOW_ROCM_LIB
+#define RTOW_ROCM_LIB "/opt/rocm/lib"
+#endif
+
 struct rtow_multi {
     std::vector<int> devices;
+    bool shared = false;  // a device listed more than once: gather by device copies, no RCCL
     std::vector<rtow_context*> ctx;
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> streams;
-    // per device: its slab (BGRA + linear); device 0 also the gathered slabs and the frame
+    // per rank: its slab (BGRA + linear); the first device also the gathered slabs and the frame
     std::vector<void*> slab_bgra, slab_lin;
-    size_t slab_px = 0;  // slab capacity in pixels (every device the same)
+    size_t slab_px = 0;  // slab capacity in pixels (every rank the same)
     void* gather_bgra = nullptr;
     void* gather_lin = nullptr;
     void* frame_bgra = nullptr;
@@ -44,13 +61,59 @@ struct rtow_multi {
 
 namespace {
 
+// ---- RCCL, resolved at first use ---------------------------------------------
+struct Rccl {
+    decltype(&ncclCommInitAll) commInitAll = nullptr;
+    decltype(&ncclCommDestroy) commDestroy = nullptr;
+    decltype(&ncclGroupStart) groupStart = nullptr;
+    decltype(&ncclGroupEnd) groupEnd = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGetErrorString) errorString = nullptr;
+    std::string error;  // why loading failed
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        // librccl.so.1 first: in a process that already holds an RCCL (torch's),
+        // the dynamic linker returns that one rather than loading a second
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen(RTOW_ROCM_LIB "/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            r.error = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+            return;
+        }
+        bool ok = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn) {
+                ok = false;
+                r.error += std::string(r.error.empty() ? "" : ", ") + "no symbol " + name;
+            }
+        };
+        sym(r.commInitAll, "ncclCommInitAll");
+        sym(r.commDestroy, "ncclCommDestroy");
+        sym(r.groupStart, "ncclGroupStart");
+        sym(r.groupEnd, "ncclGroupEnd");
+        sym(r.send, "ncclSend");
+        sym(r.recv, "ncclRecv");
+        sym(r.errorString, "ncclGetErrorString");
+        if (!ok) r.commInitAll = nullptr;  // unusable
+    });
+    return r;
+}
+
 int hip_fail(hipError_t e, const char* what) {
     return set_error(RTOW_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
 int nccl_fail(ncclResult_t r, const char* what) {
+    const Rccl& R = rccl();
     return set_error(RTOW_E_RCCL, std::string(what) + ": ncclResult " + std::to_string((int)r) + " (" +
-                                      ncclGetErrorString(r) + ")");
+                                      (R.errorString ? R.errorString(r) : "?") + ")");
 }
 
 #define MHIP(expr)                                         \
@@ -80,7 +143,7 @@ void release(rtow_multi* m) {
     m->gather_bgra = m->gather_lin = m->frame_bgra = m->frame_lin = nullptr;
     m->slab_px = m->frame_px = 0;
     for (ncclComm_t c : m->comms)
-        if (c) (void)ncclCommDestroy(c);
+        if (c) (void)rccl().commDestroy(c);
     m->comms.clear();
     for (size_t i = 0; i < m->streams.size(); i++) {
         if (!m->streams[i]) continue;
@@ -93,7 +156,7 @@ void release(rtow_multi* m) {
     m->ctx.clear();
 }
 
-// (re)size the slabs for a W x H frame split over the devices
+// (re)size the slabs for a W x H frame split over the ranks
 int ensure_buffers(rtow_multi* m, uint32_t W, uint32_t H) {
     const uint32_t n = (uint32_t)m->devices.size();
     const size_t need_px = (size_t)rtow_rank_tile_count(W, H, 0, n) * 64;  // rank 0 holds the most tiles
@@ -127,28 +190,42 @@ int ensure_buffers(rtow_multi* m, uint32_t W, uint32_t H) {
     return RTOW_OK;
 }
 
-// One gather of every device's slab (BGRA, and linear when asked) to device 0:
-// grouped point-to-point, device i's slab (its rank's tile count x 64 pixels)
-// into slot i of the gathered buffer (slab_px pixels per slot).
+// One gather of every rank's slab (BGRA, and linear when asked) to the first
+// device: rank i's slab (its tile count x 64 pixels) into slot i of the
+// gathered buffer (slab_px pixels per slot).
 int gather(rtow_multi* m, uint32_t W, uint32_t H, bool linear) {
     const uint32_t n = (uint32_t)m->devices.size();
-    MNCCL(ncclGroupStart());
+    if (m->shared) {  // ranks sharing a device: device copies on the first device's stream
+        MHIP(hipSetDevice(m->devices[0]));
+        for (uint32_t i = 0; i < n; i++) {
+            const size_t px = (size_t)rtow_rank_tile_count(W, H, i, n) * 64;
+            MHIP(hipMemcpyPeerAsync((uint8_t*)m->gather_bgra + (size_t)i * m->slab_px * 4, m->devices[0],
+                                    m->slab_bgra[i], m->devices[i], px * 4, m->streams[0]));
+            if (linear)
+                MHIP(hipMemcpyPeerAsync((float*)m->gather_lin + (size_t)i * m->slab_px * 3, m->devices[0],
+                                        m->slab_lin[i], m->devices[i], px * 12, m->streams[0]));
+        }
+        MHIP(hipStreamSynchronize(m->streams[0]));
+        return RTOW_OK;
+    }
+    const Rccl& R = rccl();
+    MNCCL(R.groupStart());
     for (uint32_t i = 0; i < n; i++) {
         const size_t px = (size_t)rtow_rank_tile_count(W, H, i, n) * 64;
-        ncclResult_t r = ncclSend(m->slab_bgra[i], px * 4, ncclUint8, 0, m->comms[i], m->streams[i]);
-        if (r == ncclSuccess && linear) r = ncclSend(m->slab_lin[i], px * 3, ncclFloat32, 0, m->comms[i], m->streams[i]);
+        ncclResult_t r = R.send(m->slab_bgra[i], px * 4, ncclUint8, 0, m->comms[i], m->streams[i]);
+        if (r == ncclSuccess && linear) r = R.send(m->slab_lin[i], px * 3, ncclFloat32, 0, m->comms[i], m->streams[i]);
         if (r == ncclSuccess)
-            r = ncclRecv((uint8_t*)m->gather_bgra + (size_t)i * m->slab_px * 4, px * 4, ncclUint8, (int)i, m->comms[0],
-                         m->streams[0]);
+            r = R.recv((uint8_t*)m->gather_bgra + (size_t)i * m->slab_px * 4, px * 4, ncclUint8, (int)i, m->comms[0],
+                       m->streams[0]);
         if (r == ncclSuccess && linear)
-            r = ncclRecv((float*)m->gather_lin + (size_t)i * m->slab_px * 3, px * 3, ncclFloat32, (int)i, m->comms[0],
-                         m->streams[0]);
+            r = R.recv((float*)m->gather_lin + (size_t)i * m->slab_px * 3, px * 3, ncclFloat32, (int)i, m->comms[0],
+                       m->streams[0]);
         if (r != ncclSuccess) {
-            (void)ncclGroupEnd();
+            (void)R.groupEnd();
             return nccl_fail(r, "ncclSend/ncclRecv (slab gather)");
         }
     }
-    MNCCL(ncclGroupEnd());
+    MNCCL(R.groupEnd());
     for (uint32_t i = 0; i < n; i++) {
         MHIP(hipSetDevice(m->devices[i]));
         MHIP(hipStreamSynchronize(m->streams[i]));
@@ -164,18 +241,20 @@ int rtow_multi_create(const int* devices, uint32_t n, rtow_multi** out) {
     if (!out) return set_error(RTOW_E_INVALID, "NULL out");
     *out = nullptr;
     if (!devices || n == 0) return set_error(RTOW_E_INVALID, "no devices");
+    bool shared = false;
     for (uint32_t i = 0; i < n; i++) {
         if (devices[i] < 0) return set_error(RTOW_E_INVALID, "negative device index");
-        for (uint32_t j = 0; j < i; j++)
-            if (devices[j] == devices[i]) return set_error(RTOW_E_INVALID, "device listed twice");
+        for (uint32_t j = 0; j < i; j++) shared |= devices[j] == devices[i];
     }
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
         return set_error(RTOW_E_NO_DEVICE, "no HIP device visible");
     for (uint32_t i = 0; i < n; i++)
         if (devices[i] >= count) return set_error(RTOW_E_INVALID, "device out of range");
+    if (!shared && !rccl().commInitAll) return set_error(RTOW_E_RCCL, rccl().error);
     auto* m = new rtow_multi;
     m->devices.assign(devices, devices + n);
+    m->shared = shared;
     m->ctx.assign(n, nullptr);
     m->slab_bgra.assign(n, nullptr);
     m->slab_lin.assign(n, nullptr);
@@ -194,11 +273,13 @@ int rtow_multi_create(const int* devices, uint32_t n, rtow_multi** out) {
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->streams[i], hipStreamNonBlocking);
         if (e != hipSuccess) return fail(hip_fail(e, "hipStreamCreateWithFlags"));
     }
-    m->comms.assign(n, nullptr);
-    const ncclResult_t r = ncclCommInitAll(m->comms.data(), (int)n, devices);
-    if (r != ncclSuccess) {
+    if (!shared) {
         m->comms.assign(n, nullptr);
-        return fail(nccl_fail(r, "ncclCommInitAll"));
+        const ncclResult_t r = rccl().commInitAll(m->comms.data(), (int)n, devices);
+        if (r != ncclSuccess) {
+            m->comms.assign(n, nullptr);
+            return fail(nccl_fail(r, "ncclCommInitAll"));
+        }
     }
     *out = m;
     return RTOW_OK;
@@ -240,8 +321,8 @@ int rtow_multi_render(rtow_multi* m, const rtow_camera* cam, const rtow_params* 
     int rc = ensure_buffers(m, W, H);
     if (rc) return rc;
     const bool linear = linear_out != nullptr;
-    // every device renders its rank's tiles at once (a render call returns
-    // when its device is done, so one host thread per device)
+    // every rank renders its tiles at once (a render call returns when its
+    // work is done, so one host thread per rank)
     std::vector<int> rcs(n, RTOW_OK);
     std::vector<std::string> errs(n);
     std::vector<rtow_stats> st(n);
@@ -251,6 +332,7 @@ int rtow_multi_render(rtow_multi* m, const rtow_camera* cam, const rtow_params* 
             rtow_params q = *p;
             q.rank = i;
             q.world = n;
+            q.flags |= RTOW_FLAG_FRAME_PLAN;  // rtow_render's chunks: the same frame for any n
             rcs[i] = rtow_render_tiles_device(m->ctx[i], cam, &q, m->slab_bgra[i], linear ? m->slab_lin[i] : nullptr,
                                               m->streams[i], &st[i]);
             if (rcs[i]) errs[i] = rtow_last_error();  // the message is thread-local
@@ -258,7 +340,8 @@ int rtow_multi_render(rtow_multi* m, const rtow_camera* cam, const rtow_params* 
     }
     for (auto& w : workers) w.join();
     for (uint32_t i = 0; i < n; i++)
-        if (rcs[i]) return set_error(rcs[i], "device " + std::to_string(m->devices[i]) + ": " + errs[i]);
+        if (rcs[i]) return set_error(rcs[i], "rank " + std::to_string(i) + " (device " + std::to_string(m->devices[i]) +
+                                                 "): " + errs[i]);
     rc = gather(m, W, H, linear);
     if (rc) return rc;
     rc = rtow_assemble_device(m->ctx[0], W, H, n, m->gather_bgra, (uint32_t)m->slab_px, m->frame_bgra, m->streams[0]);

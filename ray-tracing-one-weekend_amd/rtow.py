@@ -221,6 +221,7 @@ def check(rc, where):
 
 FLAG_STATS = 1 << 0
 FLAG_CAMERA_DOF = 1 << 1  # CAMERA_DOF_EN 1 (camera.h:124-126)
+FLAG_FRAME_PLAN = 1 << 2  # every rank chunks its samples as the whole frame does (rtow_render's sums)
 
 
 def params(width, height, spp, seed=1, **kw):
@@ -449,8 +450,10 @@ class Context:
 
 
 class Multi:
-    """rtow_multi: several GPUs from one process (device i renders rank i of n,
-    one RCCL gather to the first device, which assembles the frame)."""
+    """rtow_multi: several GPUs from one process (entry i of `devices` renders
+    rank i of n, one gather to the first device -- RCCL when the devices are
+    distinct, device copies when one is listed more than once -- which
+    assembles the frame; equal to rtow_render's frame bit for bit)."""
 
     def __init__(self, devices):
         devs = (ctypes.c_int * len(devices))(*devices)
@@ -465,14 +468,18 @@ class Multi:
     def upload(self, scene):
         check(lib().rtow_multi_upload(self._h, scene.view_ptr), "rtow_multi_upload")
 
-    def render(self, cam, p, linear=True):
-        """(bgra[H,W,4], linear[H,W,3] or None, Stats, [per-device Stats])."""
-        bgra = np.zeros((p.height, p.width, 4), np.uint8)
-        lin = np.zeros((p.height, p.width, 3), np.float32) if linear else None
+    def render(self, cam, p, linear=True, host=True):
+        """(bgra[H,W,4], linear[H,W,3] or None, Stats, [per-device Stats]).
+        host=False: the frame stays on the first device (no copy out; bgra and
+        linear are None), as bench.py --inproc times it."""
+        bgra = np.zeros((p.height, p.width, 4), np.uint8) if host else None
+        lin = np.zeros((p.height, p.width, 3), np.float32) if linear and host else None
         st = Stats()
         dst = (Stats * self.n)()
-        check(lib().rtow_multi_render(self._h, ctypes.byref(cam), ctypes.byref(p), bgra.ctypes.data,
-                                      lin.ctypes.data if linear else None, ctypes.byref(st), dst), "rtow_multi_render")
+        check(lib().rtow_multi_render(self._h, ctypes.byref(cam), ctypes.byref(p),
+                                      bgra.ctypes.data if bgra is not None else None,
+                                      lin.ctypes.data if lin is not None else None, ctypes.byref(st), dst),
+              "rtow_multi_render")
         return bgra, lin, st, list(dst)
 
     def close(self):

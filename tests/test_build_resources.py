@@ -78,7 +78,15 @@ def test_default_kernels_scratch_bounded(kernels):
         seen.add(p["MODE"])
         assert k["scratch"] <= SCRATCH_BOUND[p["MODE"]], (p, k["scratch"])
         assert k["vgpr"] <= 128, p
-    assert seen == {0, 2, 3, 4, 5, 6, 7, 8}
+    assert seen == built_modes(kernels)
+
+
+def built_modes(kernels):
+    """The MODEs the default build holds: 0, 2-6, 8; 7 (the 4-wide tree) only in
+    an EXPERIMENTS=1 build (measured slower, not shipped by default)."""
+    modes = {codeobj.demangled_params(k["name"])["MODE"] for k in kernels if codeobj.demangled_params(k["name"])}
+    assert {0, 2, 3, 4, 5, 6, 8} <= modes <= {0, 2, 3, 4, 5, 6, 7, 8}
+    return modes
 
 
 def test_each_kernel_compiled_once(kernels):
@@ -86,5 +94,4 @@ def test_each_kernel_compiled_once(kernels):
     host unit declares them extern): no instantiation is compiled twice."""
     names = [k["name"] for k in kernels]
     assert len(names) == len(set(names))
-    modes = {codeobj.demangled_params(n)["MODE"] for n in names if codeobj.demangled_params(n)}
-    assert modes == {0, 2, 3, 4, 5, 6, 7, 8}
+    built_modes(kernels)

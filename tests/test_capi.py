@@ -90,8 +90,6 @@ def test_multi_gpu_arguments_are_validated_before_any_gpu_call():
     i32 = ctypes.c_int
     assert L.rtow_multi_create(None, 1, ctypes.byref(h)) == rtow.E_INVALID
     assert L.rtow_multi_create((i32 * 1)(0), 0, ctypes.byref(h)) == rtow.E_INVALID
-    assert L.rtow_multi_create((i32 * 2)(0, 0), 2, ctypes.byref(h)) == rtow.E_INVALID  # listed twice
-    assert b"twice" in L.rtow_last_error()
     assert L.rtow_multi_create((i32 * 2)(0, -1), 2, ctypes.byref(h)) == rtow.E_INVALID
     assert L.rtow_multi_create((i32 * 1)(0), 1, None) == rtow.E_INVALID
     assert h.value is None
@@ -105,4 +103,36 @@ def test_multi_gpu_arguments_are_validated_before_any_gpu_call():
     if rtow.device_count() == 0:
         rc = L.rtow_multi_create((i32 * 2)(0, 1), 2, ctypes.byref(h))
         assert rc == rtow.E_NO_DEVICE and h.value is None
+        # a device listed twice is two ranks sharing it (no RCCL): still a device call
+        assert L.rtow_multi_create((i32 * 2)(0, 0), 2, ctypes.byref(h)) == rtow.E_NO_DEVICE
     assert L.rtow_error_string(rtow.E_RCCL) == b"RCCL error"
+
+
+def test_library_loads_without_rccl():
+    """librtow_hip.so does not link RCCL: rtow_multi opens librccl.so.1 at the
+    first rtow_multi_create that needs it, so single-GPU callers
+    load the library (and the ctypes binding) without RCCL present."""
+    import subprocess
+
+    out = subprocess.run(["readelf", "-d", rtow.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    needed = [line for line in out.splitlines() if "NEEDED" in line]
+    assert needed and not any("rccl" in line for line in needed), needed
+
+
+@pytest.mark.parametrize("W,H,spp,world", [(1920, 1080, 1024, 8), (1920, 1080, 256, 2), (4096, 4096, 8192, 8),
+                                           (800, 800, 4096, 4), (61, 45, 8, 3)])
+def test_frame_plan_flag_gives_every_rank_the_whole_frames_chunks(W, H, spp, world):
+    """RTOW_FLAG_FRAME_PLAN: a rank of any world cuts its samples as rtow_render
+    cuts the whole frame's (rank 0 of 1), so chunk float sums -- and the
+    assembled frame -- do not depend on the world size; without it a rank's
+    share plans for its own pixel count (config 2 at 8 ranks: 32-sample items
+    against the frame's 128)."""
+    whole = rtow.plan(rtow.params(W, H, spp))
+    for rank in range(world):
+        pl = rtow.plan(rtow.params(W, H, spp, rank=rank, world=world, flags=rtow.FLAG_FRAME_PLAN))
+        assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail, pl.n_chunks) == \
+               (whole.samples_per_chunk, whole.n_big, whole.tail_samples, whole.n_tail, whole.n_chunks)
+        assert pl.n_local_px == rtow.rank_tile_count(W, H, rank, world) * 64
+    own = rtow.plan(rtow.params(W, H, spp, rank=0, world=world))
+    if (W, H, spp, world) in ((1920, 1080, 1024, 8), (1920, 1080, 256, 2)):
+        assert own.samples_per_chunk < whole.samples_per_chunk  # the flag matters here

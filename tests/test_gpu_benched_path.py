@@ -92,3 +92,55 @@ def test_config5_rank_share_128_sample_items(gpu_ctx):
     assert np.isfinite(lin).all()
     assert (rms <= RMS_TOL).all(), rms
     assert n_off <= int(1e-5 * 500)
+
+
+@pytest.mark.parametrize("scene", ["cornell", "cornell_smoke"])
+def test_configs_3_4_bench_frame_4096spp(scene, gpu_ctx):
+    """Configs 3 and 4 exactly as benched: 800x800x4096,
+    one rank, automatic chunking -- 128-sample items, n_big 31, a 128-sample
+    halving tail in 8 chunks, each chunk's samples summed in float in sample
+    order (main.cpp:939-955) through MODE 5's top-level scan (hitableList.h:
+    20-38) and, for cornell_smoke, the medium (constantMedium.h:26-74).  1000
+    random pixels of the frame vs the oracle at 4096 spp; then 8 random whole
+    tiles rendered alone (rank t of world = the frame's tile count, with
+    RTOW_FLAG_FRAME_PLAN: the bench's chunks) must give the frame's values bit
+    for bit and the oracle's segment count on those 512 pixels exactly."""
+    import torch
+
+    W, H, spp = 800, 800, 4096
+    sc = rtow.Scene.build(scene, n=1, image="none", scene_seed=1)
+    cam, p, idx, lin, st, pl = _slab_render(gpu_ctx, sc, W, H, spp, 1, 0, 1)
+    assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail) == (128, 31, 128, 8), pl.as_dict()
+    assert st.samples == W * H * spp
+    rms, d, oc = _compare(sc, cam, p, idx, lin, 1000, 3)
+    n_off = int((d > 1e-3).sum())
+    frame = np.zeros((W * H, 3), np.float32)
+    ok = idx >= 0
+    frame[idx[ok]] = lin[ok]
+    # whole tiles alone: the segment count of 512 pixels, and the same values
+    n_tiles = rtow.tile_count(W, H)
+    tiles = np.random.default_rng(4).choice(n_tiles, size=8, replace=False)
+    segs, pix, vals = 0, [], []
+    bgra = torch.zeros(64 * 4, dtype=torch.uint8, device="cuda")
+    tl = torch.zeros(64 * 3, dtype=torch.float32, device="cuda")
+    for t in tiles:
+        q = rtow.params(W, H, spp, seed=1, rank=int(t), world=n_tiles, flags=rtow.FLAG_FRAME_PLAN)
+        qs = gpu_ctx.render_tiles_device(cam, q, bgra.data_ptr(), tl.data_ptr())
+        torch.cuda.synchronize()
+        ti = rtow.rank_pixels(W, H, int(t), n_tiles)
+        assert (ti >= 0).all() and qs.pixels == 64
+        segs += qs.segments
+        pix.append(ti)
+        vals.append(tl.cpu().numpy().reshape(64, 3))
+    pix, vals = np.concatenate(pix), np.concatenate(vals)
+    assert np.array_equal(vals.view(np.uint32), frame[pix].view(np.uint32))
+    _, _, tc = sio.oracle_render(sc.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                 sio.RtowParams.from_buffer_copy(bytes(p)), pixels=pix.astype(np.uint32), threads=16)
+    print(f"BENCHED {scene} 800x800x4096: plan {pl.as_dict()} rms {rms} max|d| {d.max():.3g} pixels>1e-3 "
+          f"{n_off}/1000 bit-identical {float(np.mean(d == 0)):.4f} rays/sample gpu {st.segments / st.samples:.4f} "
+          f"oracle-sample {oc.segments / oc.samples:.4f}; 8 tiles: segments gpu {segs} oracle {tc.segments} "
+          f"kernel {st.kernel_ms:.1f} ms")
+    assert np.isfinite(lin).all()
+    assert (rms <= RMS_TOL).all(), rms
+    assert d.max() <= 1e-3
+    assert segs == tc.segments

@@ -287,6 +287,16 @@ def test_grazing_box_edges_follow_the_reference(tree):
         ctx.close()
 
 
+def _wide_built():
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
+    import codeobj
+
+    return any((codeobj.demangled_params(k["name"]) or {}).get("MODE") == 7 for k in codeobj.kernels(rtow.LIB_PATH))
+
+
+@pytest.mark.skipif(not _wide_built(), reason="MODE 7 (4-wide tree) is built only with make EXPERIMENTS=1")
 @pytest.mark.parametrize("wide,spec", [("4", "0"), ("3", "0"), ("4", "16")])
 def test_wide_tree_gives_the_same_frame(wide, spec):
     """The 4-wide tree of the simple scene (MODE 7, opt-in RTOW_WIDE=k: nodes of

@@ -95,3 +95,39 @@ def test_reference_world_renders_as_product_path(scene, n, image, tmp_path, gpu_
     assert json.loads(r.stdout.strip().splitlines()[-1])["segments"] == st.segments
     assert np.array_equal(lin_d.view(np.uint32), lin.reshape(H, W, 3).view(np.uint32))
     assert np.array_equal(bgra_d, bgra.reshape(H, W, 4))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="oracle/_ref/ref_dropin not built (needs /root/reference)")
+@pytest.mark.parametrize("scene,n,image,ranks", [("random_ned", 487, "synthetic", 0), ("final_ned", 1, "synthetic", 0),
+                                                 ("cornell_smoke", 1, "none", 3)])
+def test_reference_multi_gpu_binding(scene, n, image, ranks, tmp_path, gpu_ctx):
+    """INTEGRATION.md's multi-GPU binding run from inside the reference's own
+    translation unit (oracle/_ref/ref_dropin `dropin_multi`): rtow_render_devices
+    over every visible device (ranks 0: the RCCL gather, ncclCommInitAll over
+    the devices) or over device 0 listed `ranks` times (device-copy gather).
+    No torch in that process, so the RCCL it opens is ROCm's own librccl.so.1
+    (it prints the mapped path).  The frame equals the product path's
+    rtow_render bit for bit."""
+    W, H, spp, seed = 120, 72, 8, 29
+    env = dict(os.environ, RTOW_SCENE_SEED="1")
+    pre = str(tmp_path / "m")
+    cmd = [DROPIN, "dropin_multi", scene, str(W), str(H), str(spp), pre, "--n", str(n), "--seed", str(seed),
+           "--cwd", _stage(tmp_path, image)]
+    if ranks:
+        cmd += ["--ranks", str(ranks)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    print("dropin_multi", scene, info)
+    if ranks:
+        assert info["ranks"] == ranks
+    else:
+        assert info["ranks"] == info["devices_visible"] >= 1
+        assert info["librccl"].endswith("librccl.so") and "torch" not in info["librccl"], info
+    sc = rtow.Scene.build(scene, n=n, image=image, scene_seed=1)
+    gpu_ctx.upload(sc)
+    bgra, lin, st = gpu_ctx.render(rtow.camera_main(W, H), rtow.params(W, H, spp, seed=seed))
+    assert info["segments"] == st.segments
+    assert np.array_equal(np.fromfile(pre + ".lin", np.float32).view(np.uint32), lin.reshape(-1).view(np.uint32))
+    assert np.array_equal(np.fromfile(pre + ".bgra", np.uint8), bgra.reshape(-1))
