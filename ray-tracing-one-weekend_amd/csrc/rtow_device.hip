@@ -87,6 +87,11 @@ __device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]);
 #ifndef RTOW_EXPERIMENTS
 #define RTOW_EXPERIMENTS 0
 #endif
+// RTOW_REORDER=1 (A/B experiment): the bench kernel sorts its wave's rays by
+// direction octant before the traversal
+#ifndef RTOW_REORDER
+#define RTOW_REORDER 0
+#endif
 
 // Scene records read through the constant address space: the scene is
 // read-only for a kernel's lifetime, and a load whose address is uniform
@@ -2757,10 +2762,53 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 else
                     prim = trace_wide<STACK, BS, false>(S, wnodes, S.wide_root, lray, 0.001f, bt, stk, overflow);
             } else {
+#if RTOW_REORDER
+                // (experiment) the wave's rays sorted by
+                // direction octant before the traversal: lane p traverses the
+                // ray of rank p (octant, then lane) for its owner, moved by
+                // ds_permute, and the owner pulls (bt, prim) back from lane p
+                const unsigned long long act = __ballot(1);
+                uint32_t pos = lane;
+                Ray tray = lray;
+                if (act == ~0ull) {
+                    const uint32_t oct = (lray.d.x < 0.0f ? 1u : 0u) | (lray.d.y < 0.0f ? 2u : 0u) |
+                                         (lray.d.z < 0.0f ? 4u : 0u);
+                    pos = 0;
+#pragma unroll
+                    for (uint32_t k = 0; k < 8; k++) {
+                        const unsigned long long m = __ballot(oct == k);
+                        pos += k < oct ? (uint32_t)__popcll(m)
+                                       : (k == oct ? (uint32_t)__popcll(m & ((1ull << lane) - 1ull)) : 0u);
+                    }
+                    const int addr = (int)(pos * 4u);
+                    auto push = [&](float v) {
+                        return __int_as_float(__builtin_amdgcn_ds_permute(addr, __float_as_int(v)));
+                    };
+                    tray.o = f3(push(lray.o.x), push(lray.o.y), push(lray.o.z));
+                    tray.d = f3(push(lray.d.x), push(lray.d.y), push(lray.d.z));
+                    tray.time = push(lray.time);
+                }
+                const bool tfast = dot(tray.d, tray.d) >= 0x1p-24f;
+                float tbt = FLT_MAX;
+                uint32_t tprim;
+                if (tfast)
+                    tprim = trace_simple<STACK, BS, PROF, true>(S, nodes, S.bvh_root, tray, 0.001f, tbt, stk, overflow, prof);
+                else
+                    tprim = trace_simple<STACK, BS, PROF, false>(S, nodes, S.bvh_root, tray, 0.001f, tbt, stk, overflow, prof);
+                (void)fast;
+                if (act == ~0ull) {
+                    bt = __shfl(tbt, (int)pos);
+                    prim = __shfl(tprim, (int)pos);
+                } else {
+                    bt = tbt;
+                    prim = tprim;
+                }
+#else
                 if (fast)
                     prim = trace_simple<STACK, BS, PROF, true>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
                 else
                     prim = trace_simple<STACK, BS, PROF, false>(S, nodes, S.bvh_root, lray, 0.001f, bt, stk, overflow, prof);
+#endif
             }
             hit = (prim >> KIND_SHIFT) != DK_NONE;
             if constexpr (PROF) {
