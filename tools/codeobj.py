@@ -133,3 +133,38 @@ if __name__ == "__main__":
         p = demangled_params(k["name"])
         print(p or k["name"][:40], {x: k[x] for x in ("vgpr", "scratch", "vgpr_spill", "sgpr_spill", "dyn_stack",
                                                        "lds", "calls")})
+
+
+def disasm(path, want):
+    """The disassembly (text) of the kernel whose demangled template
+    parameters equal `want` (a dict, e.g. {"MODE": 8, "STACK": 16, "WAVES": 4,
+    "PROF": 0, "BS": 256, "LDSN": 0, "DBG": 0})."""
+    for obj in code_objects(path):
+        with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as f:
+            f.write(obj)
+            co = f.name
+        try:
+            meta = _kernel_metadata(co)
+            names = [n for n in meta if demangled_params(n) == want]
+            if not names:
+                continue
+            dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co],
+                                 capture_output=True, text=True, check=True).stdout
+        finally:
+            os.unlink(co)
+        out, on = [], False
+        for line in dis.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+            if m:
+                on = m.group(1) == names[0]
+            if on:
+                out.append(line)
+        return "\n".join(out)
+    return None
+
+
+if __name__ == "__main__":  # python tools/codeobj.py LIB MODE STACK [WAVES BS LDSN] > kernel.s
+    a = sys.argv
+    want = {"MODE": int(a[2]), "STACK": int(a[3]), "WAVES": int(a[4]) if len(a) > 4 else 4, "PROF": 0,
+            "BS": int(a[5]) if len(a) > 5 else 256, "LDSN": int(a[6]) if len(a) > 6 else 0, "DBG": 0}
+    print(disasm(a[1], want))
