@@ -87,6 +87,11 @@ __device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]);
 #ifndef RTOW_EXPERIMENTS
 #define RTOW_EXPERIMENTS 0
 #endif
+// RTOW_GRID_SPEC=1 (A/B experiment): grid_walk queues a second candidate
+// per lane while the wave still walks
+#ifndef RTOW_GRID_SPEC
+#define RTOW_GRID_SPEC 0
+#endif
 // RTOW_REORDER=1 (A/B experiment): the bench kernel sorts its wave's rays by
 // direction octant before the traversal
 #ifndef RTOW_REORDER
@@ -724,6 +729,16 @@ __device__ __forceinline__ bool box6_nearest(const DevScene& S, uint32_t bi, con
     return f;
 }
 
+// Words of COLD path state per lane of the general kernels (see lds_bytes):
+// 14; 17 with a stack of 16 (MODE 5 / 8 park the sample's RNG key and counter
+// there too, PARK_RNG): either way 4 blocks of 256 fit a CU's 160 KB.
+constexpr int cold_words(int STACK) { return STACK <= 16 ? 17 : 14; }
+// MODE 8 at STACK 16 stages the grids' packed cell heights (DevScene::gq) in
+// LDS after the COLD words when they fit in this many words (4 blocks of 256
+// threads then take 4 x 40 KB of the CU's 160 KB); larger tables, and the
+// deeper-stack kernels, read them from global memory.
+[[maybe_unused]] constexpr uint32_t GRID_LDS_WORDS = 512;
+
 // Diagnostic counters (instrumented kernel variant only; see RTOW_PROFILE)
 struct Prof {
     uint32_t lane_steps, wave_steps, leaf_tests, lane_iters, wave_iters, pad;
@@ -774,11 +789,28 @@ __device__ __forceinline__ void grid_band_w(float lo, float hi, float o, float i
     t0 = flat ? (in ? -INFINITY : INFINITY) : fminf(a, b);
     t1 = flat ? (in ? INFINITY : -INFINITY) : fmaxf(a, b);
 }
-template <bool PROF = false>
+// A cell's (or row's) extent along ah from its packed word in DevScene::gq:
+// 16-bit steps of (hhi - hlo) / 65535 from the grid's hlo, rounded outward
+// (the host checks the decoded floats contain the true extent), low half the
+// lower bound.  GLDS: the words staged in LDS (lq), else global memory.
+template <bool GLDS>
+__device__ __forceinline__ void grid_ext(const DevScene& S, const uint32_t* lq, uint32_t k, float base, float step,
+                                         float& lo, float& hi) {
+    uint32_t w;
+    if constexpr (GLDS) {
+        w = lq[k];
+    } else {
+        w = S.gq[k];
+    }
+    lo = fmaf((float)(w & 0xffffu), step, base);
+    hi = fmaf((float)(w >> 16), step, base);
+}
+template <bool PROF = false, bool GLDS = false>
 __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const Ray& r, const F3& inv, float tmin,
-                                          float& bt, uint32_t& best, Prof* prof = nullptr) {
+                                          float& bt, uint32_t& best, const uint32_t* lq, Prof* prof = nullptr) {
     constexpr float REL = 0x1p-18f;
     const DGrid G = cld(S.grid + gi);
+    const float qstep = (G.hhi - G.hlo) * (1.0f / 65535.0f);  // (the host quantised with this very float)
     const uint32_t au = G.axes & 3u, av = (G.axes >> 2) & 3u, ah = (G.axes >> 4) & 3u;
     const float ou = comp(r.o, au), ov = comp(r.o, av), oh = comp(r.o, ah);
     const float du = comp(r.d, au), dv = comp(r.d, av), dh = comp(r.d, ah);
@@ -820,72 +852,139 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
     int i = 0, ncells = 0, jr = 0;
     float ra = 0.0f, rb = 0.0f;
     bool found = false, live = nrows > 0;
-    while (live) {
-        uint32_t cand = ~0u;
-        while (true) {  // this lane's next cell to scan
-            if constexpr (PROF) {  // (instrumented kernel: walk steps, lanes / wave)
-                prof->lane_steps++;
-                if (first_active_lane()) prof->wave_steps++;
+    // One walk step: the next row's set-up (falling through to its first
+    // cell) or the next cell of the row.  Returns the cell when it is a
+    // candidate (its clipped entry t in ct), else ~0u; clears `live` as soon
+    // as the walk is over -- the rows are used up, or the row ended beyond
+    // the record and the next row starts beyond it too (that check in the
+    // same step, not a step of its own).  Every step uses up a row or a cell.
+    auto step = [&](float& ct) -> uint32_t {
+        const float bound = cull_bound(bt);
+        if (ncells <= 0) {
+            if (nrows <= 0) {
+                live = false;
+                return ~0u;
             }
-            const float bound = cull_bound(bt);
-            if (ncells <= 0) {
+            const float vlo = fmaf((float)j, G.wv, G.v0);
+            float t0, t1;
+            grid_band_w(vlo - Ev, vlo + G.wv + Ev, ov, iv, vflat, t0, t1);
+            jr = j;
+            j += sv;
+            nrows--;
+            if (t0 > bound && !vflat) {  // this row and the later ones lie beyond the record
+                live = false;
+                return ~0u;
+            }
+            ra = fmaxf(t0, te);
+            rb = fminf(fminf(t1, tx), bound);
+            if (!(ra <= rb)) return ~0u;
+            {  // the row's columns span [hlo, hhi] together (row record after the cells)
+                float rlo, rhi;
+                grid_ext<GLDS>(S, lq, G.cell0 + G.nu * G.nv + (uint32_t)jr, G.hlo, qstep, rlo, rhi);
+                const float ha = fmaf(ra, dh, oh), hb = fmaf(rb, dh, oh);
+                if (fmaxf(ha, hb) + Eh < rlo || fminf(ha, hb) - Eh > rhi) return ~0u;
+            }
+            // the row's cells: u over [ra, rb], widened
+            const float ua = fmaf(ra, du, ou), ub = fmaf(rb, du, ou);
+            const float fa = floorf((fminf(ua, ub) - Eu - G.u0) * G.iwu);
+            const float fb = floorf((fmaxf(ua, ub) + Eu - G.u0) * G.iwu);
+            const int ia = (int)fminf(fmaxf(fa, 0.0f), fnu), ib = (int)fminf(fmaxf(fb, 0.0f), fnu);
+            i = su > 0 ? ia : ib;
+            ncells = ib - ia + 1;
+            // (on to the row's first cell in the same step)
+        }
+        const int ic = i;
+        i += su;
+        ncells--;
+        const float ulo = fmaf((float)ic, G.wu, G.u0);
+        float c0, c1;
+        grid_band_w(ulo - Eu, ulo + G.wu + Eu, ou, iu, uflat, c0, c1);
+        c0 = fmaxf(c0, ra);
+        c1 = fminf(fminf(c1, rb), bound);
+        if (!(c0 <= c1)) {
+            if (c0 > bound && !uflat) {  // the rest of the row lies beyond the record
+                ncells = 0;
                 if (nrows <= 0) {
                     live = false;
-                    break;
+                } else if (!vflat) {  // and the next row?
+                    const float vlo = fmaf((float)j, G.wv, G.v0);
+                    float t0, t1;
+                    grid_band_w(vlo - Ev, vlo + G.wv + Ev, ov, iv, vflat, t0, t1);
+                    if (t0 > bound) live = false;
                 }
-                const float vlo = fmaf((float)j, G.wv, G.v0);
-                float t0, t1;
-                grid_band_w(vlo - Ev, vlo + G.wv + Ev, ov, iv, vflat, t0, t1);
-                jr = j;
-                j += sv;
-                nrows--;
-                if (t0 > bound && !vflat) {  // this row and the later ones lie beyond the record
-                    live = false;
-                    break;
-                }
-                ra = fmaxf(t0, te);
-                rb = fminf(fminf(t1, tx), bound);
-                if (!(ra <= rb)) continue;
-                {  // the row's columns span [hlo, hhi] together (row record after the cells)
-                    const DGridCell R = S.gcell[G.cell0 + G.nu * G.nv + (uint32_t)jr];
-                    const float ha = fmaf(ra, dh, oh), hb = fmaf(rb, dh, oh);
-                    if (fmaxf(ha, hb) + Eh < R.hlo || fminf(ha, hb) - Eh > R.hhi) continue;
-                }
-                // the row's cells: u over [ra, rb], widened
-                const float ua = fmaf(ra, du, ou), ub = fmaf(rb, du, ou);
-                const float fa = floorf((fminf(ua, ub) - Eu - G.u0) * G.iwu);
-                const float fb = floorf((fmaxf(ua, ub) + Eu - G.u0) * G.iwu);
-                const int ia = (int)fminf(fmaxf(fa, 0.0f), fnu), ib = (int)fminf(fmaxf(fb, 0.0f), fnu);
-                i = su > 0 ? ia : ib;
-                ncells = ib - ia + 1;
-                // (on to the row's first cell in the same step)
             }
-            const int ic = i;
-            i += su;
-            ncells--;
-            const float ulo = fmaf((float)ic, G.wu, G.u0);
-            float c0, c1;
-            grid_band_w(ulo - Eu, ulo + G.wu + Eu, ou, iu, uflat, c0, c1);
-            c0 = fmaxf(c0, ra);
-            c1 = fminf(fminf(c1, rb), bound);
-            if (!(c0 <= c1)) {
-                if (c0 > bound && !uflat) ncells = 0;  // the rest of the row lies beyond the record
-                continue;
-            }
-            const DGridCell C = S.gcell[G.cell0 + (uint32_t)jr * G.nu + (uint32_t)ic];
-            const float ha = fmaf(c0, dh, oh), hb = fmaf(c1, dh, oh);
-            if (fmaxf(ha, hb) + Eh < C.hlo || fminf(ha, hb) - Eh > C.hhi) continue;
-            cand = C.box6;
-            break;
+            return ~0u;
         }
+        const uint32_t cell = G.cell0 + (uint32_t)jr * G.nu + (uint32_t)ic;
+        float clo, chi;
+        grid_ext<GLDS>(S, lq, cell, G.hlo, qstep, clo, chi);
+        const float ha = fmaf(c0, dh, oh), hb = fmaf(c1, dh, oh);
+        if (fmaxf(ha, hb) + Eh < clo || fminf(ha, hb) - Eh > chi) return ~0u;
+        ct = c0;
+        return cell;
+    };
+#if RTOW_GRID_SPEC
+    // The scans are batched: the wave walks until every live lane holds a
+    // candidate, then scans them together.  While the wave still walks, a lane
+    // that holds one walks on and queues a second (cell indices are < 2^16,
+    // GRID_LDS_WORDS: both in one register), scanned in the next batch unless
+    // the first one's hit has put it beyond the record.
+    uint32_t cq = ~0u;  // first candidate | second << 16 (0xffff: none)
+    float c2t = 0.0f;
+    while (true) {
+        while (__any(live && (cq & 0xffffu) == 0xffffu)) {
+            if (live && (cq >> 16) == 0xffffu) {
+                if constexpr (PROF) {  // (instrumented kernel: walk steps, lanes / wave)
+                    prof->lane_steps++;
+                    if (first_active_lane()) prof->wave_steps++;
+                }
+                float ct;
+                const uint32_t c = step(ct);
+                if (c != ~0u) {
+                    if ((cq & 0xffffu) == 0xffffu) {
+                        cq = 0xffff0000u | c;
+                    } else {
+                        cq = (cq & 0xffffu) | c << 16;
+                        c2t = ct;
+                    }
+                }
+            }
+        }
+        if (!__any((cq & 0xffffu) != 0xffffu)) break;
+        if ((cq & 0xffffu) != 0xffffu) {
+            if constexpr (PROF) {
+                prof->box_lanes++;
+                if (first_active_lane()) prof->box_waves++;
+            }
+            if (box6_scan(S, S.gcell[cq & 0xffffu].box6, r, inv, tmin, bt, best)) found = true;
+        }
+        cq = (cq >> 16) != 0xffffu && c2t <= cull_bound(bt) ? 0xffff0000u | cq >> 16 : ~0u;
+    }
+#else
+    // The scans are batched: the wave walks until every live lane holds a
+    // candidate (or has ended its walk), then scans them together.
+    while (true) {
+        uint32_t cand = ~0u;
+        while (__any(live && cand == ~0u)) {
+            if (live && cand == ~0u) {
+                if constexpr (PROF) {  // (instrumented kernel: walk steps, lanes / wave)
+                    prof->lane_steps++;
+                    if (first_active_lane()) prof->wave_steps++;
+                }
+                float ct;
+                cand = step(ct);
+            }
+        }
+        if (!__any(cand != ~0u)) break;
         if (cand != ~0u) {
             if constexpr (PROF) {
                 prof->box_lanes++;
                 if (first_active_lane()) prof->box_waves++;
             }
-            if (box6_scan(S, cand, r, inv, tmin, bt, best)) found = true;
+            if (box6_scan(S, S.gcell[cand].box6, r, inv, tmin, bt, best)) found = true;
         }
     }
+#endif
     return found;
 }
 
@@ -1855,7 +1954,10 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
         } else if (kind == TOP_DTREE) {
             trace_dnodes<STACK, true>(S, T.a, r, inv, a, ra, tmin, bt, bp, stk, overflow);
         } else if (GRID && kind == TOP_GRID) {
-            grid_walk<PROF>(S, T.a, r, inv, tmin, bt, bp, prof);
+            // (the packed heights staged after the COLD words: STACK 16 only)
+            constexpr bool GLDS = STACK <= 16;
+            grid_walk<PROF, GLDS>(S, T.a, r, inv, tmin, bt, bp,
+                                  stk - threadIdx.x + (size_t)(STACK + cold_words(STACK)) * BLOCK, prof);
         } else if (kind == TOP_SPHERE) {
             const Sph sp = load_sph(S.sph + T.a);
             const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
@@ -2624,7 +2726,6 @@ __device__ __forceinline__ float fx_value(unsigned long long l0, unsigned long l
 // (the general kernels are register-bound: 128 VGPRs at 4 waves/SIMD).
 // 14 words; 17 with a stack of 16 (MODE 5 parks the sample's RNG key and
 // counter there too, PARK_RNG): either way 4 blocks of 256 fit a CU's 160 KB.
-constexpr int cold_words(int STACK) { return STACK <= 16 ? 17 : 14; }
 template <int MODE, int STACK>
 constexpr bool park_rng() { return (MODE == 5 || MODE == 8) && STACK <= 16; }
 
@@ -2648,6 +2749,10 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
     for (uint32_t i = threadIdx.x; i < 256; i += BS) {
         s_ranvec[i] = reinterpret_cast<const float4*>(S.ranvec)[i];
         s_perm[i] = S.perm[i];
+    }
+    if constexpr (MODE == 8 && STACK <= 16) {  // the grids' packed heights (grid_walk, GLDS)
+        uint32_t* lq = reinterpret_cast<uint32_t*>(smem + 5120 + (size_t)(STACK + cold_words(STACK)) * BS * 4);
+        for (uint32_t i = threadIdx.x; i < S.n_gq; i += BS) lq[i] = S.gq[i];
     }
     const DNode* nodes = S.node;
     const DWide* wnodes = S.wide;
@@ -3178,6 +3283,7 @@ struct HostLayout {
     std::vector<DBox6> box6;         // DevScene::box6
     std::vector<DGrid> grid;         // DevScene::grid (TOP_GRID)
     std::vector<DGridCell> gcell;    // DevScene::gcell
+    std::vector<uint32_t> gq;        // DevScene::gq: gcell's extents packed (grid_ext), one word each
     std::unordered_map<uint32_t, uint32_t> grid_of;  // a grid's BvhNode ref -> its DGrid
     uint32_t grid_top = 0;           // TOP_GRID items of the top-level list (DevScene::n_grid)
     float tshift[3] = {0.0f, 0.0f, 0.0f};  // DevScene::tshift
@@ -3827,6 +3933,29 @@ struct GeneralSah {
         return onlyUnitSpheres(L.bvh[idx].left, depth + 1) && onlyUnitSpheres(L.bvh[idx].right, depth + 1);
     }
 
+    // grid_ext's packed extents: 16-bit steps of (hhi - hlo) / 65535 (that
+    // float, as the kernel computes it) from the grid's hlo, the lower bound
+    // rounded down and the upper up (one step more either way); false if a
+    // decoded float (fmaf, as the kernel decodes) does not contain the true
+    // extent -- then the grid is not used and its tree is traversed instead.
+    static bool packHeights(const DGrid& g, const std::vector<DGridCell>& cells, std::vector<uint32_t>& out) {
+        const float step = (g.hhi - g.hlo) * (1.0f / 65535.0f);
+        out.clear();
+        for (const DGridCell& c : cells) {
+            uint32_t q[2];
+            for (int e = 0; e < 2; e++) {
+                const double h = e ? c.hhi : c.hlo;
+                double x = step > 0.0f ? (h - (double)g.hlo) / (double)step : 0.0;
+                x = e ? std::ceil(x) + 1.0 : std::floor(x) - 1.0;
+                q[e] = (uint32_t)std::min(65535.0, std::max(0.0, x));
+            }
+            const float lo = std::fmaf((float)q[0], step, g.hlo), hi = std::fmaf((float)q[1], step, g.hlo);
+            if (!(lo <= c.hlo && hi >= c.hhi)) return false;
+            out.push_back(q[0] | q[1] << 16);
+        }
+        return true;
+    }
+
     // A BvhNode whose leaves are Boxes (rectangle lists with a DBox6), all in
     // one frame, that tile a regular grid of columns along two axes (one Box
     // per cell, within a 2^-12 cell width of the cell; any extent along the
@@ -3898,6 +4027,10 @@ struct GeneralSah {
                 cells[c] = DGridCell{q.lo[ah], q.hi[ah], b, 0u};
             }
             if (!ok) continue;
+            // the cell and row extents as packed 16-bit words (gq), staged in
+            // LDS by the MODE 8 kernel: the whole table must fit, and the
+            // decoded floats must contain every true extent
+            if (L.gcell.size() + (size_t)nu * nv + nv > GRID_LDS_WORDS) continue;
             DGrid g{};
             g.u0 = u0, g.v0 = v0, g.wu = (float)wu, g.wv = (float)wv;
             g.iwu = (float)(1.0 / wu), g.iwv = (float)(1.0 / wv);
@@ -3906,15 +4039,19 @@ struct GeneralSah {
             g.axes = au | av << 2 | ah << 4;
             g.cell0 = (uint32_t)L.gcell.size();
             g.margin = (float)(std::max(wu, wv) * 0x1p-10);  // 2^2 x the tolerance above
-            L.gcell.insert(L.gcell.end(), cells.begin(), cells.end());
+            std::vector<DGridCell> all(cells);
             for (uint32_t j = 0; j < nv; j++) {  // per row: the extent of its columns together
                 DGridCell row{FLT_MAX, -FLT_MAX, 0u, 0u};
                 for (uint32_t i = 0; i < nu; i++) {
                     row.hlo = std::min(row.hlo, cells[(size_t)j * nu + i].hlo);
                     row.hhi = std::max(row.hhi, cells[(size_t)j * nu + i].hhi);
                 }
-                L.gcell.push_back(row);
+                all.push_back(row);
             }
+            std::vector<uint32_t> packed;
+            if (!packHeights(g, all, packed)) continue;
+            L.gcell.insert(L.gcell.end(), all.begin(), all.end());
+            L.gq.insert(L.gq.end(), packed.begin(), packed.end());
             L.grid_of[ref] = (uint32_t)L.grid.size();
             L.grid.push_back(g);
             return true;
@@ -5262,7 +5399,8 @@ int ensure(void** p, size_t* have, size_t need) {
 template <int MODE, int STACK, int WAVES, bool PROF = false, int BS = BLOCK, bool LDSN = false, bool DBG = false>
 int launchTrace(rtow_context* c, const DevCam& cam, const DevParams& P, uint32_t bpc, hipStream_t st) {
     const size_t lds = lds_bytes(STACK, BS, MODE == 7 ? 2u * c->scene.n_wide : c->scene.n_node, LDSN,
-                                 MODE != 0 && MODE != 7);
+                                 MODE != 0 && MODE != 7) +
+                       (MODE == 8 && STACK <= 16 ? (size_t)c->scene.n_gq * 4u : 0u);
     // the occupancy query is host work between the launch events: once per
     // (kernel, LDS size) per process
     static std::mutex mu;
@@ -5749,7 +5887,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     const uint32_t n_grid = L.grid_top;
     if (L.grid.empty()) L.grid.push_back(DGrid{});
     if (L.gcell.empty()) L.gcell.push_back(DGridCell{});
-    size_t o_grid = pushBlob(blob, L.grid), o_gcell = pushBlob(blob, L.gcell);
+    const uint32_t n_gq = (uint32_t)L.gq.size();
+    if (L.gq.empty()) L.gq.push_back(0u);
+    size_t o_grid = pushBlob(blob, L.grid), o_gcell = pushBlob(blob, L.gcell), o_gq = pushBlob(blob, L.gq);
     if (L.xh.empty()) L.xh.push_back(XHit{});
     if (L.xrefs.empty()) L.xrefs.push_back(0u);
     size_t o_xh = pushBlob(blob, L.xh), o_xrefs = pushBlob(blob, L.xrefs);
@@ -5795,6 +5935,8 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.box6 = (const DBox6*)(b + o_box6);
     d.grid = (const DGrid*)(b + o_grid);
     d.gcell = (const DGridCell*)(b + o_gcell);
+    d.gq = (const uint32_t*)(b + o_gq);
+    d.n_gq = n_gq;
     d.n_grid = n_grid;
     for (int a = 0; a < 3; a++) d.tshift[a] = L.tshift[a];
     d.root = L.root;

@@ -287,6 +287,8 @@ struct DevScene {
     const DBox6* box6;       // Boxes among the rectangle lists (DList::box6, TOP_BOX6, MB_BOX6)
     const DGrid* grid;       // TOP_GRID items (MODE 8)
     const DGridCell* gcell;
+    const uint32_t* gq;      // gcell's extents packed to 16-bit steps (grid_ext), staged in LDS by MODE 8
+    uint32_t n_gq;
     uint32_t n_grid;
     uint32_t n_top;
     // Per rectangle: (offset << 8) | count of the boxes (8 floats each in

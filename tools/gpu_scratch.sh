@@ -1,5 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_benched_path.py tests/test_reference_binding.py -m gpu -v -s --timeout 200 --timeout-method thread > gpurun_out/new_tests.log 2>&1 || exit $?
-AB_SPP=256 AB_ROUNDS=3 AB_SPC=0 AB_SCENES=random_ned timeout -k 10 300 python -u tools/ab.py ray-tracing-one-weekend_amd/librtow_hip.so ab/reorder/pkg/librtow_hip.so > gpurun_out/ab_reorder.txt 2>&1 || exit $?
+AB_SPP=256 AB_ROUNDS=3 AB_SPC=0 AB_SCENES=final_ned timeout -k 10 400 python -u tools/ab.py ab/base/librtow_hip.so ab/lds/librtow_hip.so ab/tail/librtow_hip.so ab/spec3/librtow_hip.so > gpurun_out/ab_grid2_r05.txt 2>&1 || exit $?
+for v in tail spec3; do
+RTOW_LIB=ab/$v/librtow_hip.so timeout -k 10 200 python -u tools/prof_counters.py final_ned 32 > gpurun_out/prof_final_ned_$v.txt 2>&1 || exit $?
+done
