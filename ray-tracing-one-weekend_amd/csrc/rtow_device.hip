@@ -87,11 +87,6 @@ __device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]);
 #ifndef RTOW_EXPERIMENTS
 #define RTOW_EXPERIMENTS 0
 #endif
-// RTOW_GRID_SPEC=1 (A/B experiment): grid_walk queues a second candidate
-// per lane while the wave still walks
-#ifndef RTOW_GRID_SPEC
-#define RTOW_GRID_SPEC 0
-#endif
 // RTOW_REORDER=1 (A/B experiment): the bench kernel sorts its wave's rays by
 // direction octant before the traversal
 #ifndef RTOW_REORDER
@@ -852,130 +847,71 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
     int i = 0, ncells = 0, jr = 0;
     float ra = 0.0f, rb = 0.0f;
     bool found = false, live = nrows > 0;
-    // One walk step: the next row's set-up (falling through to its first
-    // cell) or the next cell of the row.  Returns the cell when it is a
-    // candidate (its clipped entry t in ct), else ~0u; clears `live` as soon
-    // as the walk is over -- the rows are used up, or the row ended beyond
-    // the record and the next row starts beyond it too (that check in the
-    // same step, not a step of its own).  Every step uses up a row or a cell.
-    auto step = [&](float& ct) -> uint32_t {
-        const float bound = cull_bound(bt);
-        if (ncells <= 0) {
-            if (nrows <= 0) {
-                live = false;
-                return ~0u;
+    // (Measured, round 5: a lane that holds its candidate walking on to queue
+    // a second while the wave's slowest lane still walks raises the walk's
+    // lane efficiency from 0.22 to 0.37 but costs registers and scans: -0.3 %
+    // to -7 %; DESIGN.md "Grids of Boxes".)
+    while (live) {
+        uint32_t cand = ~0u;
+        while (true) {  // this lane's next cell to scan
+            if constexpr (PROF) {  // (instrumented kernel: walk steps, lanes / wave)
+                prof->lane_steps++;
+                if (first_active_lane()) prof->wave_steps++;
             }
-            const float vlo = fmaf((float)j, G.wv, G.v0);
-            float t0, t1;
-            grid_band_w(vlo - Ev, vlo + G.wv + Ev, ov, iv, vflat, t0, t1);
-            jr = j;
-            j += sv;
-            nrows--;
-            if (t0 > bound && !vflat) {  // this row and the later ones lie beyond the record
-                live = false;
-                return ~0u;
-            }
-            ra = fmaxf(t0, te);
-            rb = fminf(fminf(t1, tx), bound);
-            if (!(ra <= rb)) return ~0u;
-            {  // the row's columns span [hlo, hhi] together (row record after the cells)
-                float rlo, rhi;
-                grid_ext<GLDS>(S, lq, G.cell0 + G.nu * G.nv + (uint32_t)jr, G.hlo, qstep, rlo, rhi);
-                const float ha = fmaf(ra, dh, oh), hb = fmaf(rb, dh, oh);
-                if (fmaxf(ha, hb) + Eh < rlo || fminf(ha, hb) - Eh > rhi) return ~0u;
-            }
-            // the row's cells: u over [ra, rb], widened
-            const float ua = fmaf(ra, du, ou), ub = fmaf(rb, du, ou);
-            const float fa = floorf((fminf(ua, ub) - Eu - G.u0) * G.iwu);
-            const float fb = floorf((fmaxf(ua, ub) + Eu - G.u0) * G.iwu);
-            const int ia = (int)fminf(fmaxf(fa, 0.0f), fnu), ib = (int)fminf(fmaxf(fb, 0.0f), fnu);
-            i = su > 0 ? ia : ib;
-            ncells = ib - ia + 1;
-            // (on to the row's first cell in the same step)
-        }
-        const int ic = i;
-        i += su;
-        ncells--;
-        const float ulo = fmaf((float)ic, G.wu, G.u0);
-        float c0, c1;
-        grid_band_w(ulo - Eu, ulo + G.wu + Eu, ou, iu, uflat, c0, c1);
-        c0 = fmaxf(c0, ra);
-        c1 = fminf(fminf(c1, rb), bound);
-        if (!(c0 <= c1)) {
-            if (c0 > bound && !uflat) {  // the rest of the row lies beyond the record
-                ncells = 0;
+            const float bound = cull_bound(bt);
+            if (ncells <= 0) {
                 if (nrows <= 0) {
                     live = false;
-                } else if (!vflat) {  // and the next row?
-                    const float vlo = fmaf((float)j, G.wv, G.v0);
-                    float t0, t1;
-                    grid_band_w(vlo - Ev, vlo + G.wv + Ev, ov, iv, vflat, t0, t1);
-                    if (t0 > bound) live = false;
+                    break;
                 }
-            }
-            return ~0u;
-        }
-        const uint32_t cell = G.cell0 + (uint32_t)jr * G.nu + (uint32_t)ic;
-        float clo, chi;
-        grid_ext<GLDS>(S, lq, cell, G.hlo, qstep, clo, chi);
-        const float ha = fmaf(c0, dh, oh), hb = fmaf(c1, dh, oh);
-        if (fmaxf(ha, hb) + Eh < clo || fminf(ha, hb) - Eh > chi) return ~0u;
-        ct = c0;
-        return cell;
-    };
-#if RTOW_GRID_SPEC
-    // The scans are batched: the wave walks until every live lane holds a
-    // candidate, then scans them together.  While the wave still walks, a lane
-    // that holds one walks on and queues a second (cell indices are < 2^16,
-    // GRID_LDS_WORDS: both in one register), scanned in the next batch unless
-    // the first one's hit has put it beyond the record.
-    uint32_t cq = ~0u;  // first candidate | second << 16 (0xffff: none)
-    float c2t = 0.0f;
-    while (true) {
-        while (__any(live && (cq & 0xffffu) == 0xffffu)) {
-            if (live && (cq >> 16) == 0xffffu) {
-                if constexpr (PROF) {  // (instrumented kernel: walk steps, lanes / wave)
-                    prof->lane_steps++;
-                    if (first_active_lane()) prof->wave_steps++;
+                const float vlo = fmaf((float)j, G.wv, G.v0);
+                float t0, t1;
+                grid_band_w(vlo - Ev, vlo + G.wv + Ev, ov, iv, vflat, t0, t1);
+                jr = j;
+                j += sv;
+                nrows--;
+                if (t0 > bound && !vflat) {  // this row and the later ones lie beyond the record
+                    live = false;
+                    break;
                 }
-                float ct;
-                const uint32_t c = step(ct);
-                if (c != ~0u) {
-                    if ((cq & 0xffffu) == 0xffffu) {
-                        cq = 0xffff0000u | c;
-                    } else {
-                        cq = (cq & 0xffffu) | c << 16;
-                        c2t = ct;
-                    }
+                ra = fmaxf(t0, te);
+                rb = fminf(fminf(t1, tx), bound);
+                if (!(ra <= rb)) continue;
+                {  // the row's columns span [hlo, hhi] together (row record after the cells)
+                    float rlo, rhi;
+                    grid_ext<GLDS>(S, lq, G.cell0 + G.nu * G.nv + (uint32_t)jr, G.hlo, qstep, rlo, rhi);
+                    const float ha = fmaf(ra, dh, oh), hb = fmaf(rb, dh, oh);
+                    if (fmaxf(ha, hb) + Eh < rlo || fminf(ha, hb) - Eh > rhi) continue;
                 }
+                // the row's cells: u over [ra, rb], widened
+                const float ua = fmaf(ra, du, ou), ub = fmaf(rb, du, ou);
+                const float fa = floorf((fminf(ua, ub) - Eu - G.u0) * G.iwu);
+                const float fb = floorf((fmaxf(ua, ub) + Eu - G.u0) * G.iwu);
+                const int ia = (int)fminf(fmaxf(fa, 0.0f), fnu), ib = (int)fminf(fmaxf(fb, 0.0f), fnu);
+                i = su > 0 ? ia : ib;
+                ncells = ib - ia + 1;
+                // (on to the row's first cell in the same step)
             }
-        }
-        if (!__any((cq & 0xffffu) != 0xffffu)) break;
-        if ((cq & 0xffffu) != 0xffffu) {
-            if constexpr (PROF) {
-                prof->box_lanes++;
-                if (first_active_lane()) prof->box_waves++;
+            const int ic = i;
+            i += su;
+            ncells--;
+            const float ulo = fmaf((float)ic, G.wu, G.u0);
+            float c0, c1;
+            grid_band_w(ulo - Eu, ulo + G.wu + Eu, ou, iu, uflat, c0, c1);
+            c0 = fmaxf(c0, ra);
+            c1 = fminf(fminf(c1, rb), bound);
+            if (!(c0 <= c1)) {
+                if (c0 > bound && !uflat) ncells = 0;  // the rest of the row lies beyond the record
+                continue;
             }
-            if (box6_scan(S, S.gcell[cq & 0xffffu].box6, r, inv, tmin, bt, best)) found = true;
+            const uint32_t cell = G.cell0 + (uint32_t)jr * G.nu + (uint32_t)ic;
+            float clo, chi;
+            grid_ext<GLDS>(S, lq, cell, G.hlo, qstep, clo, chi);
+            const float ha = fmaf(c0, dh, oh), hb = fmaf(c1, dh, oh);
+            if (fmaxf(ha, hb) + Eh < clo || fminf(ha, hb) - Eh > chi) continue;
+            cand = cell;
+            break;
         }
-        cq = (cq >> 16) != 0xffffu && c2t <= cull_bound(bt) ? 0xffff0000u | cq >> 16 : ~0u;
-    }
-#else
-    // The scans are batched: the wave walks until every live lane holds a
-    // candidate (or has ended its walk), then scans them together.
-    while (true) {
-        uint32_t cand = ~0u;
-        while (__any(live && cand == ~0u)) {
-            if (live && cand == ~0u) {
-                if constexpr (PROF) {  // (instrumented kernel: walk steps, lanes / wave)
-                    prof->lane_steps++;
-                    if (first_active_lane()) prof->wave_steps++;
-                }
-                float ct;
-                cand = step(ct);
-            }
-        }
-        if (!__any(cand != ~0u)) break;
         if (cand != ~0u) {
             if constexpr (PROF) {
                 prof->box_lanes++;
@@ -984,7 +920,6 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
             if (box6_scan(S, S.gcell[cand].box6, r, inv, tmin, bt, best)) found = true;
         }
     }
-#endif
     return found;
 }
 
