@@ -230,24 +230,29 @@ __device__ __forceinline__ Ray root_ray(const DevScene& S, const Ray& w) {
 }
 
 // the ray in the frame of chain `id` (DevScene::chains), outermost first
+__device__ __forceinline__ void chain_step(float4 e, Ray& r) {
+    const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
+    if (kind == DK_TRANSLATE) {
+        r.o = sub(r.o, f3(e.y, e.z, e.w));
+    } else if (kind == DK_ROTY) {  // apply_inst's operations
+        const float sn = e.y, c = e.z;
+        const F3 o = r.o, d = r.d;
+        r.o.x = c * o.x - sn * o.z;
+        r.o.z = sn * o.x + c * o.z;
+        r.d.x = c * d.x - sn * d.z;
+        r.d.z = sn * d.x + c * d.z;
+    }
+}
 __device__ __forceinline__ Ray chain_ray(const DevScene& S, uint32_t id, const Ray& w) {
     const DChainX* C = S.chains + id;
+    // the count and the first two entries in one round trip (the scan's
+    // scalar loads otherwise wait for each other: count, entry 0, entry 1, ...)
     const int n = (int)cld(&C->n);
+    const float4 e0 = cld4(C->t), e1 = cld4(C->t + 1);
     Ray r = w;
-    for (int k = 0; k < n; k++) {
-        const float4 e = cld4(C->t + k);
-        const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
-        if (kind == DK_TRANSLATE) {
-            r.o = sub(r.o, f3(e.y, e.z, e.w));
-        } else if (kind == DK_ROTY) {  // apply_inst's operations
-            const float sn = e.y, c = e.z;
-            const F3 o = r.o, d = r.d;
-            r.o.x = c * o.x - sn * o.z;
-            r.o.z = sn * o.x + c * o.z;
-            r.d.x = c * d.x - sn * d.z;
-            r.d.z = sn * d.x + c * d.z;
-        }
-    }
+    if (n > 0) chain_step(e0, r);
+    if (n > 1) chain_step(e1, r);
+    for (int k = 2; k < n; k++) chain_step(cld4(C->t + k), r);
     return r;
 }
 
@@ -257,8 +262,11 @@ __device__ __forceinline__ void inst_out(const DevScene& S, uint32_t ref, F3& p,
 // the way out of the instances, innermost first
 __device__ __forceinline__ void chain_out(const DevScene& S, uint32_t id, F3& p, F3& nrm) {
     const DChainX* C = S.chains + id;
-    for (int k = (int)cld(&C->n) - 1; k >= 0; k--) {  // inst_out's operations
-        const float4 e = cld4(C->t + k);
+    // (the count and the first two entries in one round trip, as chain_ray)
+    const int n = (int)cld(&C->n);
+    const float4 e0 = cld4(C->t), e1 = cld4(C->t + 1);
+    for (int k = n - 1; k >= 0; k--) {  // inst_out's operations
+        const float4 e = k == 0 ? e0 : (k == 1 ? e1 : cld4(C->t + k));
         const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
         if (kind == DK_FLIP) {
             nrm = neg(nrm);
@@ -4961,6 +4969,23 @@ void buildTop(HostLayout& L) {
     // in chain order: translations leave the direction alone) differ.  Items
     // the general traversal runs (TOP_GENERIC) do not use the scan's ray, and
     // the first in-place item after one recomputes it.
+    // the ray's frame: the chain's translations and rotations in order (a
+    // FlipNormals leaves the ray alone), so items under chains that differ
+    // only in flips share the scan's ray (cornell's walls: one ray for six)
+    auto raySig = [&](uint32_t c) {
+        std::vector<uint64_t> v;
+        const DChain& C = L.chains[c];
+        for (uint32_t k = 0; k < C.n; k++) {
+            const uint32_t kind = C.ref[k] >> KIND_SHIFT;
+            if (kind != DK_ROTY && kind != DK_TRANSLATE) continue;
+            const DInst& I = L.inst[C.ref[k] & INDEX_MASK];
+            uint32_t b[3];
+            std::memcpy(b, I.p, 12);
+            v.push_back((uint64_t)kind << 32 | b[0]);
+            v.push_back((uint64_t)b[1] << 32 | b[2]);
+        }
+        return v;
+    };
     auto dirSig = [&](uint32_t c) {
         std::vector<uint64_t> v;
         const DChain& C = L.chains[c];
@@ -4975,18 +5000,24 @@ void buildTop(HostLayout& L) {
         return v;
     };
     uint32_t last = ~0u;
-    std::vector<uint64_t> lastSig;
+    std::vector<uint64_t> lastSig, lastRay;
     for (DTop& t : L.top) {
         if (t.kind == TOP_GENERIC) {  // (the kernel drops the scan's ray there)
             last = ~0u;
             continue;
         }
         if (t.chain == last) continue;
+        std::vector<uint64_t> rs = raySig(t.chain);
+        if (last != ~0u && rs == lastRay) {  // another chain, the same ray
+            last = t.chain;
+            continue;
+        }
         std::vector<uint64_t> sig = dirSig(t.chain);
         t.kind |= TOP_NEWCHAIN;
         if (last == ~0u || sig != lastSig) t.kind |= TOP_NEWDIR;
         last = t.chain;
         lastSig = std::move(sig);
+        lastRay = std::move(rs);
     }
 }
 
