@@ -26,12 +26,16 @@ sys.path.insert(0, os.path.join(HERE, ".."))
 import bench  # noqa: E402
 
 
-def pmc_roofline(scene, W, H, segments, kernel_ms, src_hash):
+def pmc_roofline(scene, W, H, segments, kernel_ms, src_hash, spp=None, world=1):
     """The VALU-issue roofline of this config's trace kernel (bench.py's
-    definition): wave-instructions per ray from the newest PMC summary of the
-    same workload and frame size (profiles/*/pmc_summary.json, this build's
-    source hash preferred; its spp may be lower: VALU per ray does not depend
-    on it) x the rays of this launch / its kernel time."""
+    definition), from the newest PMC summary of the same workload and frame
+    size (profiles/*/pmc_summary.json, this build's source hash preferred).
+    One number from one launch: when the summary profiled this
+    very launch (same frame, spp and world), its VALU count per ray x this
+    launch's rays / this launch's kernel time, as bench.py prices its line;
+    otherwise (config 5: the summary is a 256-spp whole frame, this launch an
+    8192-spp share) the summary's own launch -- its VALU count / its own kernel
+    time -- with `pmc_config` naming that launch."""
     import glob
 
     best = None
@@ -54,13 +58,19 @@ def pmc_roofline(scene, W, H, segments, kernel_ms, src_hash):
         return None
     _, f, d = best
     vpr = d["SQ_INSTS_VALU"] / d["rays_per_launch"]
-    achieved = vpr * segments / (kernel_ms * 1e-3) / 1e9
+    same_launch = spp is not None and d.get("config", [None] * 5)[2] == spp and (d.get("config") + [1])[4] == world
+    if same_launch or not d.get("kernel_ms_pmc"):
+        achieved = vpr * segments / (kernel_ms * 1e-3) / 1e9
+    else:
+        achieved = d["SQ_INSTS_VALU"] / (d["kernel_ms_pmc"] * 1e-3) / 1e9
     lane = d["SQ_THREAD_CYCLES_VALU"] / (d["SQ_ACTIVE_INST_VALU"] * 64) if "SQ_THREAD_CYCLES_VALU" in d else None
     out = {"bound": "valu", "achieved": round(achieved, 1), "peak": bench.VALU_PEAK_G, "unit": "Gwave-instr/s",
            "frac": round(achieved / bench.VALU_PEAK_G, 4), "valu_per_ray": round(vpr, 3),
            "lane_util": round(lane, 4) if lane is not None else None,
            "useful_lane_frac": round(achieved / bench.VALU_PEAK_G * lane, 4) if lane is not None else None,
            "pmc": os.path.relpath(f, os.path.join(HERE, "..")), "pmc_config": d.get("config"),
+           "priced_on": "this launch" if (same_launch or not d.get("kernel_ms_pmc")) else
+                        "the PMC summary's own launch (pmc_config)",
            "pmc_matches_build": d.get("source_hash") == src_hash}
     if "WRITE_SIZE" in d:
         out["write_bytes_per_ray"] = round(d["WRITE_SIZE"] * 1024 / d["rays_per_launch"], 2)
@@ -122,7 +132,7 @@ def main():
                "segments": st.segments, "rays_per_sample": round(st.segments / max(st.samples, 1), 4),
                "seconds": round(wall, 3), "kernel_ms": round(st.kernel_ms, 2),
                "mray_per_s": round(st.segments / wall / 1e6, 2), "msample_per_s": round(st.samples / wall / 1e6, 3),
-               "roofline": pmc_roofline(name, W, H, st.segments, st.kernel_ms, rtow.source_hash()),
+               "roofline": pmc_roofline(name, W, H, st.segments, st.kernel_ms, rtow.source_hash(), spp, world),
                "cpu_baseline": cpu_rate(scene, cam, W, H, spp, args.cpu_seconds, threads)}
         if world > 1:
             out["note"] = (f"one GPU rendered rank 0's 1/{world} share; {world} GPUs render the frame in about "
