@@ -4,10 +4,15 @@ RCCL gather (ncclCommInitAll + grouped ncclSend/ncclRecv) to the first device,
 which assembles the frame.  The reference's counterpart is its N worker
 threads over a column interleave (main.cpp:182-195, 936).
 
-The test box has one GPU, so n = 1 here: device 0's slab still goes through
-RCCL (a send to itself), the assemble kernels run, and the frame must equal
-rtow_render's bit for bit.  n > 1 needs several GPUs (unmeasured here; the
-same code with more communicators)."""
+The test box has one GPU.  With distinct devices that is n = 1: device 0's
+slab still goes through RCCL (a send to itself), the assemble kernels run, and
+the frame must equal rtow_render's bit for bit.  The n-rank code -- one host
+thread per rank, the world-n slab offsets, the assembly -- runs with device 0
+listed several times (ranks sharing it, gathered by device copies) and with k
+contexts rendering ranks of world k at once; every rank chunks as the whole
+frame (RTOW_FLAG_FRAME_PLAN), so those frames equal rtow_render's bit for bit
+too.  n > 1 distinct devices (the RCCL gather between GPUs) is skipped below
+two visible GPUs."""
 import numpy as np
 import pytest
 
