@@ -101,6 +101,14 @@ def parse(argv=None):
                     help="one process drives all --gpus N devices through the C-ABI's own multi-GPU render "
                          "(rtow_multi_render: a host thread per device, one RCCL gather, assembly on device 0; "
                          "every rank chunks as the whole frame), instead of one process per GPU")
+    ap.add_argument("--share-device", action="store_true",
+                    help="(test mode, not a bench line) every rank renders on cuda:0 and the slabs are gathered "
+                         "with gloo through host memory: the multi-process path with real kernels on a one-GPU box")
+    ap.add_argument("--frame-plan", action="store_true",
+                    help="every rank chunks its samples as the whole frame (RTOW_FLAG_FRAME_PLAN): the assembled "
+                         "frame equals a one-GPU rtow_render bit for bit")
+    ap.add_argument("--dump-frame", default=None,
+                    help="rank 0 writes the last step's assembled BGRA frame (H x W x 4 bytes) to this file")
     ap.add_argument("--pmc-json", default=None,
                     help="PMC summary to use (default: the newest profiles/*/pmc_summary.json of this build+config)")
     args = ap.parse_args(argv)
@@ -303,13 +311,22 @@ def roofline(args, world, launch_rays, mean_kms, bpr, src_hash):
 
 # ---------------------------------------------------------------------------
 # one step
-def frame_step(render, assemble, slab, gathered, rank, world, dist=None):
+def frame_step(render, assemble, slab, gathered, rank, world, dist=None, host_gather=False):
     """One bench step: this rank renders its 8x8-tile slab (`render(slab)`),
     one gather brings every rank's slab to rank 0 (torch.distributed: RCCL
     over xGMI on the GPUs, gloo in tests/test_distributed.py), rank 0
-    assembles the frame (`assemble(gathered)`).  Returns render's stats."""
+    assembles the frame (`assemble(gathered)`).  host_gather: the slabs go
+    through host memory (gloo between processes sharing one GPU,
+    --share-device).  Returns render's stats."""
     st = render(slab)
-    if world > 1:
+    if world > 1 and host_gather:
+        hs = slab.cpu()
+        hg = [h.clone() for h in gathered.cpu().unbind(0)] if rank == 0 else None
+        dist.gather(hs, hg, dst=0)
+        if rank == 0:
+            for r in range(world):
+                gathered[r].copy_(hg[r])
+    elif world > 1:
         dist.gather(slab, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
     else:
         gathered[0].copy_(slab)
@@ -330,6 +347,9 @@ class HipRank:
         import rtow
 
         self.args, self.rank, self.world = args, rank, world
+        if args.share_device:  # (test mode) every rank on the one GPU, gloo between them
+            local = 0
+            self.backend = "gloo"
         torch.cuda.set_device(local)
         self.device = torch.device("cuda", local)
         W, H = args.width, args.height
@@ -342,7 +362,8 @@ class HipRank:
         self.gathered = torch.zeros((world, self.stride * 4), dtype=torch.uint8, device=self.device) if rank == 0 else None
         self.frame = torch.zeros((H, W, 4), dtype=torch.uint8, device=self.device) if rank == 0 else None
         self.stream = torch.cuda.current_stream().cuda_stream
-        self.p = rtow.params(W, H, args.spp, seed=args.seed, rank=rank, world=world)
+        self.p = rtow.params(W, H, args.spp, seed=args.seed, rank=rank, world=world,
+                             flags=rtow.FLAG_FRAME_PLAN if args.frame_plan else 0)
         # load the code objects once (not a step: the warmup steps stay the contract's)
         if not args.no_prime:
             self.ctx.render_tiles_device(self.cam, rtow.params(W, H, 1, seed=args.seed, rank=rank, world=world),
@@ -350,7 +371,7 @@ class HipRank:
         torch.cuda.synchronize()
 
     def init_kwargs(self):
-        return {"device_id": self.device}
+        return {} if self.args.share_device else {"device_id": self.device}
 
     def step(self, dist):
         W, H = self.args.width, self.args.height
@@ -358,7 +379,11 @@ class HipRank:
             lambda sl: self.ctx.render_tiles_device(self.cam, self.p, sl.data_ptr(), None, self.stream),
             lambda g: self.ctx.assemble_device(W, H, self.world, g.data_ptr(), self.stride, self.frame.data_ptr(),
                                                self.stream),
-            self.slab, self.gathered, self.rank, self.world, dist)
+            self.slab, self.gathered, self.rank, self.world, dist, host_gather=self.args.share_device)
+
+    def dump_frame(self, path):
+        if self.rank == 0:
+            self.frame.cpu().numpy().tofile(path)
 
     def sync(self):
         import torch
@@ -450,6 +475,8 @@ def run(args, make_rank):
     R = make_rank(args, rank, world, local)
     distributed = world > 1
     n_gpus = getattr(R, "n_gpus", world)  # --inproc: one process, N devices
+    if args.share_device:  # (test mode) every rank process on the one GPU
+        n_gpus = 1
     if distributed:
         dist.init_process_group(R.backend, **R.init_kwargs())
 
@@ -471,10 +498,13 @@ def run(args, make_rank):
     R.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    if getattr(args, "dump_frame", None) and hasattr(R, "dump_frame"):
+        R.dump_frame(args.dump_frame)
     mean_kms = float(np.mean(kms)) if kms else 0.0
-    tot = torch.tensor([float(segs), float(samples)], dtype=torch.float64, device=R.device)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=R.device)
-    rk = torch.tensor([mean_kms], dtype=torch.float64, device=R.device)
+    cdev = torch.device("cpu") if R.backend == "gloo" else R.device  # (gloo collectives on host tensors)
+    tot = torch.tensor([float(segs), float(samples)], dtype=torch.float64, device=cdev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    rk = torch.tensor([mean_kms], dtype=torch.float64, device=cdev)
     rank_kms = [rk.clone() for _ in range(world)]
     if distributed:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
@@ -497,6 +527,7 @@ def run(args, make_rank):
             "unit": "Mray/s",
             "msample_per_s": round(samples_all / elapsed / 1e6, 3),
             "n_gpus": n_gpus,
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / max(args.steps, 1), 2),
@@ -509,9 +540,12 @@ def run(args, make_rank):
                                     if scene == "random_ned" else f"{label} ({scene}), ")
                                    + f"{W}x{H}x{spp}spp, depth 50, synthetic 2048x1024 earth texture",
                        "scene": scene, "width": W, "height": H, "spp": spp, "n": args.n, "scene_seed": 1,
-                       "render_seed": args.seed, "baseline_config": is_baseline_cfg,
+                       "render_seed": args.seed, "baseline_config": is_baseline_cfg and not args.share_device,
                        "parallelism": (f"tiles8x8 interleaved over {n_gpus} device(s) of one process "
                                        "(rtow_multi_render: RCCL gather to device 0)" if args.inproc else
+                                       f"tiles8x8 interleaved over {world} rank processes sharing cuda:0 + gloo "
+                                       "gather through host memory (test mode, not a multi-GPU measurement)"
+                                       if args.share_device else
                                        f"tiles8x8 interleaved over {world} rank(s) + gather to rank 0")},
             "rays_per_sample": round(segs_all / max(samples_all, 1), 4),
             "rays_per_step": int(segs_all / max(args.steps, 1)),

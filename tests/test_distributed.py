@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, spp, out_path):
+def _worker(rank, world, port, W, H, spp, out_path, host_gather=False):
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -60,17 +60,19 @@ def _worker(rank, world, port, W, H, spp, out_path):
     def assemble(g):  # rtow.assemble: the numpy mirror of assemble_kernel
         np.save(out_path, rtow.assemble(g.view(world, stride, 4).numpy(), W, H, world))
 
-    cnt = bench.frame_step(render, assemble, slab, gathered, rank, world, dist)
+    cnt = bench.frame_step(render, assemble, slab, gathered, rank, world, dist, host_gather=host_gather)
     assert cnt.samples == int(valid.sum()) * spp
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("W,H", [(29, 21), (48, 48)])
-def test_gloo_world2_gather_assembles_single_rank_frame(W, H, tmp_path):
+@pytest.mark.parametrize("W,H,host_gather", [(29, 21, False), (48, 48, False), (29, 21, True)])
+def test_gloo_world2_gather_assembles_single_rank_frame(W, H, host_gather, tmp_path):
+    """host_gather: the slabs staged through host memory (bench.py
+    --share-device, ranks sharing one GPU)."""
     spp, world = 4, 2
     out = str(tmp_path / "frame.npy")
-    mp.spawn(_worker, args=(world, _free_port(), W, H, spp, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, spp, out, host_gather), nprocs=world, join=True)
     frame = np.load(out)
     scene = rtow.Scene.build("cornell_smoke")
     cam = sio.RtowCamera.from_buffer_copy(bytes(rtow.camera_main(W, H)))

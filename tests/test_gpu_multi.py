@@ -221,3 +221,36 @@ def test_multi_all_devices_equal_render(gpu_ctx):
         m.close()
     assert np.array_equal(ml.view(np.uint32), lin.view(np.uint32)) and np.array_equal(mb, bgra)
     assert mst.segments == st.segments and len(dst) == n
+
+
+def test_bench_multiprocess_ranks_sharing_the_gpu(tmp_path, gpu_ctx):
+    """bench.py's own N > 1 path with the real kernels on the one-GPU box:
+    `--gpus 2 --share-device` starts two rank processes (torch.distributed.run),
+    both render their tile slabs on cuda:0 at the same time, the slabs are
+    gathered (gloo through host memory: RCCL allows one rank per device) and
+    rank 0 assembles the frame on the GPU.  With --frame-plan the dumped frame
+    equals one GPU's rtow_render bit for bit, and the line's ray count equals
+    that render's (the one-process-per-GPU path the driver times at N > 1,
+    minus the RCCL gather)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    W, H, spp = 320, 180, 16
+    out = str(tmp_path / "frame.bgra")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--share-device", "--frame-plan",
+           "--width", str(W), "--height", str(H), "--spp", str(spp), "--steps", "2", "--warmup", "1", "--no-cpu",
+           "--dump-frame", out]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    print("share-device bench:", {k: line[k] for k in ("value", "n_gpus", "ranks", "rays_per_step", "rank_kernel_ms")})
+    assert line["ranks"] == 2 and line["n_gpus"] == 1 and len(line["rank_kernel_ms"]["per_rank"]) == 2
+    sc = rtow.Scene.build("random_ned", n=487, image="synthetic", scene_seed=1)
+    gpu_ctx.upload(sc)
+    bgra, _, st = gpu_ctx.render(rtow.camera_main(W, H), rtow.params(W, H, spp, seed=1), linear=False)
+    assert line["rays_per_step"] == st.segments
+    assert np.array_equal(np.fromfile(out, np.uint8).reshape(H, W, 4), bgra)
