@@ -87,6 +87,11 @@ __device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]);
 #ifndef RTOW_EXPERIMENTS
 #define RTOW_EXPERIMENTS 0
 #endif
+// RTOW_FIN_RT=0 (A/B): the general scenes' finalize as before round 5 (the
+// leaf's chain id, the chain, the record and its material one after another)
+#ifndef RTOW_FIN_RT
+#define RTOW_FIN_RT 1
+#endif
 // RTOW_REORDER=1 (A/B experiment): the bench kernel sorts its wave's rays by
 // direction octant before the traversal
 #ifndef RTOW_REORDER
@@ -260,29 +265,29 @@ __device__ __forceinline__ Ray chain_ray(const DevScene& S, uint32_t id, const R
 __device__ __forceinline__ void inst_out(const DevScene& S, uint32_t ref, F3& p, F3& nrm);
 
 // the way out of the instances, innermost first
+__device__ __forceinline__ void chain_out_step(float4 e, F3& p, F3& nrm) {  // inst_out's operations
+    const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
+    if (kind == DK_FLIP) {
+        nrm = neg(nrm);
+    } else if (kind == DK_TRANSLATE) {
+        p = add(p, f3(e.y, e.z, e.w));
+    } else {
+        const float sn = e.y, c = e.z;
+        F3 q = p, m = nrm;
+        q.x = c * p.x + sn * p.z;
+        q.z = -sn * p.x + c * p.z;
+        m.x = c * nrm.x + sn * nrm.z;
+        m.z = -sn * nrm.x + c * nrm.z;
+        p = q;
+        nrm = m;
+    }
+}
 __device__ __forceinline__ void chain_out(const DevScene& S, uint32_t id, F3& p, F3& nrm) {
     const DChainX* C = S.chains + id;
     // (the count and the first two entries in one round trip, as chain_ray)
     const int n = (int)cld(&C->n);
     const float4 e0 = cld4(C->t), e1 = cld4(C->t + 1);
-    for (int k = n - 1; k >= 0; k--) {  // inst_out's operations
-        const float4 e = k == 0 ? e0 : (k == 1 ? e1 : cld4(C->t + k));
-        const uint32_t kind = __float_as_uint(e.x) >> KIND_SHIFT;
-        if (kind == DK_FLIP) {
-            nrm = neg(nrm);
-        } else if (kind == DK_TRANSLATE) {
-            p = add(p, f3(e.y, e.z, e.w));
-        } else {
-            const float sn = e.y, c = e.z;
-            F3 q = p, m = nrm;
-            q.x = c * p.x + sn * p.z;
-            q.z = -sn * p.x + c * p.z;
-            m.x = c * nrm.x + sn * nrm.z;
-            m.z = -sn * nrm.x + c * nrm.z;
-            p = q;
-            nrm = m;
-        }
-    }
+    for (int k = n - 1; k >= 0; k--) chain_out_step(k == 0 ? e0 : (k == 1 ? e1 : cld4(C->t + k)), p, nrm);
 }
 
 __device__ __forceinline__ void root_out(const DevScene& S, F3& p, F3& nrm) {
@@ -1944,10 +1949,71 @@ __device__ __forceinline__ void sphere_uv(F3 p, float& u, float& v) {
 // The HitRecord of the winning leaf: the ray into the leaf's frame (its
 // instance chain), the leaf's record, then the instances' way out.
 // SIMPLE: every leaf sits under the root chain (kernel-argument registers).
-template <bool SIMPLE>
+template <bool SIMPLE, bool NEWFIN = true>
 __device__ __forceinline__ void finalize(const DevScene& S, uint32_t prim, float t, const Ray& wray, Rec& rec) {
     const uint32_t kind = prim >> KIND_SHIFT;
     const uint32_t idx = prim & INDEX_MASK;
+#if RTOW_FIN_RT
+    if constexpr (!SIMPLE && NEWFIN) {
+        // General scenes, in two memory round trips: the leaf's whole record
+        // (its chain id, material and the host's "needs uv" bit ride along:
+        // RECT_UV / SPH_UV), then the chain's count and first two entries,
+        // which serve the way in and the way out (chain_ray / chain_out).
+        float4 q0, q1, q2 = make_float4(0, 0, 0, 0);
+        if (kind == DK_SPHERE) {
+            const float4* g = reinterpret_cast<const float4*>(S.sph + idx);
+            q0 = g[0], q1 = g[1], q2 = g[2];  // c0 r | dc t0 | t1 mat moving chain
+        } else if (kind == DK_RECT) {
+            const float4* g = reinterpret_cast<const float4*>(S.rect + idx);
+            q0 = g[0], q1 = g[1];  // a0 a1 b0 b1 | k axis mat chain
+        } else {
+            const float4* g = reinterpret_cast<const float4*>(S.med + idx);
+            q0 = g[0], q1 = g[1];  // boundary phase_mat inv_density chain | ...
+        }
+        const uint32_t chain = __float_as_uint(kind == DK_SPHERE ? q2.w : (kind == DK_RECT ? q1.w : q0.w));
+        const DChainX* C = S.chains + chain;
+        const int n = (int)C->n;
+        const float4 e0 = C->t[0], e1 = C->t[1];
+        Ray r = wray;
+        if (n > 0) chain_step(e0, r);
+        if (n > 1) chain_step(e1, r);
+        for (int k = 2; k < n; k++) chain_step(C->t[k], r);
+        rec.t = t;
+        rec.u = 0.0f;
+        rec.v = 0.0f;
+        rec.p = at(r, t);
+        if (kind == DK_SPHERE) {
+            // sph_center's arithmetic ((time - 0) / (1 - 0) is time exactly)
+            const uint32_t flags = __float_as_uint(q2.z);
+            const float f = (r.time - q1.w) / (q2.x - q1.w);
+            const F3 pc = sub(rec.p, add(f3(q0.x, q0.y, q0.z), scl(f, f3(q1.x, q1.y, q1.z))));
+            const float rr = 1.0f / q0.w;
+            rec.n = f3(div_by(pc.x, q0.w, rr), div_by(pc.y, q0.w, rr), div_by(pc.z, q0.w, rr));
+            rec.mat = __float_as_uint(q2.y);
+            if (flags & SPH_UV) sphere_uv(rec.n, rec.u, rec.v);
+        } else if (kind == DK_RECT) {
+            const uint32_t axis = __float_as_uint(q1.y);
+            uint32_t i, j, k;
+            rect_axes(axis & 3u, i, j, k);
+            if (axis & RECT_UV) {  // (u, v reach nothing else: two divisions saved)
+                const float x = comp(r.o, i) + t * comp(r.d, i);
+                const float y = comp(r.o, j) + t * comp(r.d, j);
+                rec.u = (x - q0.x) / (q0.y - q0.x);
+                rec.v = (y - q0.z) / (q0.w - q0.z);
+            }
+            const float nv = (axis & RECT_FLIP) ? -1.0f : 1.0f;  // FlipNormals folded into the leaf
+            const float zero = (axis & RECT_FLIP) ? -0.0f : 0.0f;
+            rec.n = f3(k == 0 ? nv : zero, k == 1 ? nv : zero, k == 2 ? nv : zero);
+            rec.mat = __float_as_uint(q1.z);
+        } else {  // DK_MEDIUM
+            rec.n = f3(1, 0, 0);
+            rec.mat = __float_as_uint(q0.y);
+        }
+        for (int k = n - 1; k >= 0; k--)  // inst_out's operations, innermost first
+            chain_out_step(k == 0 ? e0 : (k == 1 ? e1 : C->t[k]), rec.p, rec.n);
+        return;
+    }
+#endif
     const uint32_t chain =
         SIMPLE ? 0u : (kind == DK_SPHERE ? S.sph[idx].chain : (kind == DK_RECT ? S.rect[idx].chain : S.med[idx].chain));
     const Ray r = SIMPLE ? root_ray(S, wray) : chain_ray(S, chain, wray);
@@ -1961,7 +2027,8 @@ __device__ __forceinline__ void finalize(const DevScene& S, uint32_t prim, float
         const float rr = 1.0f / s.r;
         rec.n = f3(div_by(pc.x, s.r, rr), div_by(pc.y, s.r, rr), div_by(pc.z, s.r, rr));
         rec.mat = s.mat;
-        if (!s.moving && S.mat[s.mat].needs_uv) sphere_uv(rec.n, rec.u, rec.v);
+        // (general scenes carry SPH_UV above the moving bit)
+        if ((SIMPLE ? !s.moving : !(s.moving & 1u)) && S.mat[s.mat].needs_uv) sphere_uv(rec.n, rec.u, rec.v);
     } else if (kind == DK_RECT) {
         const DRect& q = S.rect[idx];
         uint32_t i, j, k;
@@ -2926,7 +2993,8 @@ __global__ __launch_bounds__(BS, WAVES) void trace_kernel(DevScene S, DevCam C, 
                 rng.ctr = cold[12 * BS];  // same draws (the key is the sample's)
                 hit = xhit(S, P, ray, 0.001f, rng, rec, overflow);
             } else if (hit) {
-                finalize<false>(S, best.prim & ~TIE_MASK, best.t, ray, rec);
+                finalize<false, RTOW_FIN_RT == 1 || (RTOW_FIN_RT == 2 && MODE == 8)>(S, best.prim & ~TIE_MASK, best.t,
+                                                                                       ray, rec);
             }
             acc = f3(__uint_as_float(cold[0 * BS]), __uint_as_float(cold[1 * BS]), __uint_as_float(cold[2 * BS]));
             thr = f3(__uint_as_float(cold[3 * BS]), __uint_as_float(cold[4 * BS]), __uint_as_float(cold[5 * BS]));
@@ -5289,6 +5357,14 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH, ui
             if ((t.kind & TOP_KIND_MASK) == TOP_MEDIUM) top_med[t.a] = true;
         for (size_t i = 0; i < L.med.size(); i++)
             if (!top_med[i]) L.media_nested = true;
+    }
+    // finalize's "needs uv" bits (general scenes: finalize<false> reads them
+    // from the leaf's own record instead of loading its material)
+    if (!L.simple) {
+        for (DRect& q : L.rect)
+            if (q.mat < L.mat.size() && L.mat[q.mat].needs_uv) q.axis |= RECT_UV;
+        for (DSphere& q : L.sph)
+            if (!q.moving && q.mat < L.mat.size() && L.mat[q.mat].needs_uv) q.moving |= SPH_UV;
     }
     if (L.sph_key.empty()) L.sph_key.push_back(0);
     if (L.rect_key.empty()) L.rect_key.push_back(0);

@@ -112,6 +112,11 @@ struct alignas(16) DSphere {  // 48 B
 // axis & RECT_FLIP: a FlipNormals directly above the rectangle (hitable.h:28-36)
 // folded into the leaf.
 constexpr uint32_t RECT_FLIP = 4u;
+// finalize's "needs uv" bits, set once the materials are known (buildLayout):
+// DRect::axis & RECT_UV, DSphere::moving & SPH_UV (a static sphere whose
+// material reads (u, v)); bit 0 of DSphere::moving stays "moving"
+constexpr uint32_t RECT_UV = 8u;
+constexpr uint32_t SPH_UV = 2u;
 struct alignas(16) DRect {  // 32 B
     float a0, a1, b0, b1;
     float k;
