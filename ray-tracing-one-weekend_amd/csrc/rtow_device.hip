@@ -92,6 +92,11 @@ __device__ __forceinline__ F3 ld3(const float* p) { return f3(p[0], p[1], p[2]);
 #ifndef RTOW_FIN_RT
 #define RTOW_FIN_RT 1
 #endif
+// RTOW_TEX_RT=0 (A/B): texture values through the material's texture record
+// and a checker's child records (before round 5)
+#ifndef RTOW_TEX_RT
+#define RTOW_TEX_RT 1
+#endif
 // RTOW_REORDER=1 (A/B experiment): the bench kernel sorts its wave's rays by
 // direction octant before the traversal
 #ifndef RTOW_REORDER
@@ -2583,6 +2588,37 @@ __device__ __forceinline__ F3 texture_at(const DevScene& S, const Tables& T, con
                                          const Rec& rec, uint32_t depth, uint32_t* wave_stack) {
     uint32_t ti = 0;
     bool need = false;
+#if RTOW_TEX_RT
+    // a constant colour inline in the material, or a checker of two constant
+    // colours inline in its record: no further texture record to load
+    bool have = false;
+    F3 cv = f3(0, 0, 0);
+    if (hit) {
+        const DMat m = S.mat[rec.mat];
+        need = m.kind == RTOW_MAT_DIFFUSE_LIGHT ||
+               ((m.kind == RTOW_MAT_LAMBERTIAN || m.kind == RTOW_MAT_ISOTROPIC) && depth < P.max_depth);
+        if (need && m.tex == TEX_INLINE) {
+            have = true;
+            cv = f3(m.albedo[0], m.albedo[1], m.albedo[2]);
+        } else if (need) {
+            ti = m.tex;
+            for (int guard = 0; guard < 32; guard++) {  // resolve_tex, flattened checkers taken inline
+                const DTex t = S.tex[ti];
+                if (t.kind != RTOW_TEX_CHECKER) break;
+                const float sines = sinf(10 * rec.p.x) * sinf(10 * rec.p.y) * sinf(10 * rec.p.z);  // texture.h:27-35
+                if (t.c & TEX_FLAT) {
+                    have = true;
+                    cv = sines < 0 ? f3(t.f[0], t.f[1], t.f[2]) : f3(t.g[0], t.g[1], t.g[2]);
+                    break;
+                }
+                ti = sines < 0 ? t.a : t.b;
+            }
+        }
+    }
+    const bool noise = need && !have && S.tex[ti].kind == RTOW_TEX_NOISE;
+    const float turb = wave_turbulence<BS>(T, wave_stack, noise, rec.p);
+    return need ? (have ? cv : leaf_tex_value(S, ti, rec.u, rec.v, rec.p, turb)) : f3(0, 0, 0);
+#else
     if (hit) {
         const uint32_t kind = S.mat[rec.mat].kind;
         need = kind == RTOW_MAT_DIFFUSE_LIGHT ||
@@ -2592,6 +2628,7 @@ __device__ __forceinline__ F3 texture_at(const DevScene& S, const Tables& T, con
     const bool noise = need && S.tex[ti].kind == RTOW_TEX_NOISE;
     const float turb = wave_turbulence<BS>(T, wave_stack, noise, rec.p);
     return need ? leaf_tex_value(S, ti, rec.u, rec.v, rec.p, turb) : f3(0, 0, 0);
+#endif
 }
 
 // The rest of one color() call (color.h:12-59) after the closest hit:
@@ -5228,16 +5265,37 @@ int buildLayout(const rtow_scene& s, HostLayout& L, int tree = RTOW_TREE_SAH, ui
             return set_error(RTOW_E_INVALID, "texture index out of range");
         d.needs_uv = (m.kind == RTOW_MAT_METAL || m.kind == RTOW_MAT_DIELECTRIC) ? 0u
                                                                                  : (textureNeedsUv(s, m.texture) ? 1u : 0u);
+#if RTOW_TEX_RT
+        // a constant texture's colour inline (one record less to load per hit)
+        if ((m.kind == RTOW_MAT_LAMBERTIAN || m.kind == RTOW_MAT_DIFFUSE_LIGHT || m.kind == RTOW_MAT_ISOTROPIC) &&
+            s.textures[m.texture].kind == RTOW_TEX_CONSTANT) {
+            d.tex = TEX_INLINE;
+            for (int a = 0; a < 3; a++) d.albedo[a] = s.textures[m.texture].f[a];
+        }
+#endif
         L.mat.push_back(d);
     }
     for (uint32_t i = 0; i < s.n_textures; i++) {
         DTex d{};
-        std::memcpy(&d, &s.textures[i], sizeof d);
+        std::memcpy(&d, &s.textures[i], sizeof(rtow_texture));
         if (d.kind == RTOW_TEX_IMAGE && d.a >= s.n_images) return set_error(RTOW_E_INVALID, "image index out of range");
         if (d.kind == RTOW_TEX_CHECKER && (d.a >= s.n_textures || d.b >= s.n_textures))
             return set_error(RTOW_E_INVALID, "checker child out of range");
         L.tex.push_back(d);
     }
+#if RTOW_TEX_RT
+    // checkers of two constant textures: both colours inline (texture_at)
+    for (DTex& d : L.tex) {
+        if (d.kind != RTOW_TEX_CHECKER || s.textures[d.a].kind != RTOW_TEX_CONSTANT ||
+            s.textures[d.b].kind != RTOW_TEX_CONSTANT)
+            continue;
+        d.c = TEX_FLAT;
+        for (int a = 0; a < 3; a++) {
+            d.f[a] = s.textures[d.a].f[a];
+            d.g[a] = s.textures[d.b].f[a];
+        }
+    }
+#endif
     L.ranvec.resize(256 * 4);
     L.perm.resize(256);
     for (int i = 0; i < 256; i++) {

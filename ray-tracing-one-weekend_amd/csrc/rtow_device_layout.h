@@ -266,10 +266,17 @@ struct alignas(16) DMat {  // 32 B
     float albedo[3];
 };
 
-struct alignas(16) DTex {  // 32 B (rtow_texture)
+struct alignas(16) DTex {  // 48 B: rtow_texture (32 B), then g
     uint32_t kind, a, b, c;
     float f[4];
+    float g[4];  // a CHECKER whose two textures are CONSTANT (c & TEX_FLAT): odd colour in f, even in g
 };
+// DTex::c of a CheckerTexture: its odd / even colours inline (texture_at), no
+// further texture record to load
+constexpr uint32_t TEX_FLAT = 1u;
+// DMat::tex of a Lambertian / DiffuseLight / Isotropic whose texture is a
+// ConstantTexture: the colour is inline in DMat::albedo (texture_at)
+constexpr uint32_t TEX_INLINE = 0xffffffffu;
 
 struct alignas(16) DImage {
     uint32_t nx, ny;
