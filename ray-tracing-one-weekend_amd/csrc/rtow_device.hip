@@ -935,7 +935,7 @@ __device__ __forceinline__ bool grid_walk(const DevScene& S, uint32_t gi, const 
                 prof->box_lanes++;
                 if (first_active_lane()) prof->box_waves++;
             }
-            if (box6_scan(S, S.gcell[cand].box6, r, inv, tmin, bt, best)) found = true;
+            if (box6_scan(S, G.box0 + (cand - G.cell0), r, inv, tmin, bt, best)) found = true;
         }
     }
     return found;
@@ -4098,6 +4098,14 @@ struct GeneralSah {
             }
             std::vector<uint32_t> packed;
             if (!packHeights(g, all, packed)) continue;
+            // the cells' Boxes copied in cell order (the walk computes a
+            // candidate's DBox6 instead of loading its index); a copy's first
+            // side is the same rectangle, so its tie keys are the Box's
+            g.box0 = (uint32_t)L.box6.size();
+            for (size_t c = 0; c < cells.size(); c++) {
+                const DBox6 b = L.box6[cells[c].box6];
+                L.box6.push_back(b);
+            }
             L.gcell.insert(L.gcell.end(), all.begin(), all.end());
             L.gq.insert(L.gq.end(), packed.begin(), packed.end());
             L.grid_of[ref] = (uint32_t)L.grid.size();

@@ -251,7 +251,7 @@ struct alignas(16) DGrid {  // 64 B
     uint32_t axes;    // au | av << 2 | ah << 4
     uint32_t cell0;
     float margin;     // spatial widening of every cell (and of the grid's box)
-    uint32_t pad;
+    uint32_t box0;    // cell (i, j)'s Box is DBox6 box0 + j nu + i (copies in cell order: no index load)
 };
 struct alignas(16) DGridCell {  // 16 B
     float hlo, hhi;  // the Box's extent along ah
