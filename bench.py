@@ -465,7 +465,23 @@ class InprocRank(HipRank):
 def run(args, make_rank):
     """The timed loop of every rank: W warmup steps, then exactly K steps
     between barrier + device synchronize on both sides; the whole-job rate is
-    all ranks' rays over the slowest rank's time.  Rank 0 prints the line."""
+    all ranks' rays over the slowest rank's time.  Rank 0 prints the line.
+
+    Only that line goes to stdout: the process's fd 1 points at stderr while
+    the run lasts (RCCL prints its version banner to stdout when it creates a
+    communicator), and the line is written to the original stdout."""
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        _run(args, make_rank, line_fd)
+    finally:
+        sys.stdout.flush()
+        os.dup2(line_fd, 1)
+        os.close(line_fd)
+
+
+def _run(args, make_rank, line_fd):
     import torch
     import torch.distributed as dist
 
@@ -552,7 +568,7 @@ def run(args, make_rank):
             "rank_kernel_ms": {"min": min(per_rank), "max": max(per_rank), "per_rank": per_rank},
         }
         out.update(R.report(segs, args.steps, mean_kms))
-        print(json.dumps(out), flush=True)
+        os.write(line_fd, (json.dumps(out) + "\n").encode())
     R.close()
     if distributed:
         dist.destroy_process_group()
