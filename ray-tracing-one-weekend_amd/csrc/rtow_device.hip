@@ -1912,10 +1912,21 @@ __device__ __forceinline__ bool traverse_top(const DevScene& S, const Ray& wray,
             grid_walk<PROF, GLDS>(S, T.a, r, inv, tmin, bt, bp,
                                   stk - threadIdx.x + (size_t)(STACK + cold_words(STACK)) * BLOCK, prof);
         } else if (kind == TOP_SPHERE) {
-            const Sph sp = load_sph(S.sph + T.a);
-            const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
-            float t;
-            if (sph_root(c, sp.r * sp.r, r, a, ra, tmin, t)) take_hit(S, t, bt, bp, mkref(DK_SPHERE, T.a));
+            if constexpr (GRID) {  // grid worlds: a run of spheres in this frame (copies: chain = own index)
+                for (uint32_t k = 0; k < T.b; k++) {
+                    const DSphere* q = S.tsph + T.a + k;
+                    const Sph sp = load_sph(q);
+                    const uint32_t si = cld(&q->chain);
+                    const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
+                    float t;
+                    if (sph_root(c, sp.r * sp.r, r, a, ra, tmin, t)) take_hit(S, t, bt, bp, mkref(DK_SPHERE, si));
+                }
+            } else {
+                const Sph sp = load_sph(S.sph + T.a);
+                const F3 c = S.unit_time ? sph_center<true>(sp, r.time) : sph_center<false>(sp, r.time);
+                float t;
+                if (sph_root(c, sp.r * sp.r, r, a, ra, tmin, t)) take_hit(S, t, bt, bp, mkref(DK_SPHERE, T.a));
+            }
         }
     }
     if constexpr (PROF) {
@@ -3318,6 +3329,7 @@ struct HostLayout {
     std::vector<unsigned long long> sph_key, rect_key, med_key;
     std::vector<DChain> chains;
     std::vector<DTop> top;
+    std::vector<DSphere> tsph;       // grid worlds: copies of the top-level spheres, by run (DevScene::tsph)
     std::vector<float> bvh_own;      // 6 per reference BvhNode slot: its own box (bvhNode.h:58)
     // n == 1 BvhNodes (collapsed into their leaf): the leaf's ref -> index of
     // the node's own box (6 floats) in collapsed_own; AABB::hit still tests it
@@ -5077,6 +5089,35 @@ void buildTop(HostLayout& L) {
                                              : DTop{TOP_GENERIC, item, 0, list_chain};
         }
     }
+    // in grid worlds (the MODE 8 kernels), runs of top-level spheres in one
+    // frame become one item: the scan tests them in a loop over copies in
+    // DevScene::tsph (the copy's `chain` holds the sphere's own index, for
+    // the record and its tie key), one descriptor load and one dispatch for
+    // the run instead of one per sphere.  (A/B, frames identical: final_ned
+    // +2.8%; the loop in the MODE 5 kernel cost cornell / cornell_smoke 0.3 /
+    // 0.8%, so those keep one item per sphere.)
+    if (L.grid_top) {
+        std::vector<DTop> merged;
+        for (size_t q = 0; q < L.top.size();) {
+            const DTop t = L.top[q];
+            if (t.kind != TOP_SPHERE) {
+                merged.push_back(t);
+                q++;
+                continue;
+            }
+            size_t e = q;
+            while (e < L.top.size() && L.top[e].kind == TOP_SPHERE && L.top[e].chain == t.chain) e++;
+            DTop m{TOP_SPHERE, (uint32_t)L.tsph.size(), (uint32_t)(e - q), t.chain};
+            for (size_t k = q; k < e; k++) {
+                DSphere c = L.sph[L.top[k].a];
+                c.chain = L.top[k].a;
+                L.tsph.push_back(c);
+            }
+            merged.push_back(m);
+            q = e;
+        }
+        L.top = std::move(merged);
+    }
     // where the scan's ray changes (traverse_top): a new frame, and a new
     // direction when the frames' rotations (their RotateY sines and cosines,
     // in chain order: translations leave the direction alone) differ.  Items
@@ -6004,6 +6045,9 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     const uint32_t n_wide = (uint32_t)L.wide.size();
     if (L.wide.empty()) L.wide.push_back(DWide{});
     size_t o_wide = pushBlob(blob, L.wide);
+    if (!L.tsph.empty() && n_wide)  // (DevScene::wide / tsph share a slot: simple / grid worlds)
+        return set_error(RTOW_E_INVALID, "internal: a 4-wide tree in a grid world");
+    const size_t o_tsph = L.tsph.empty() ? o_wide : pushBlob(blob, L.tsph);
     HIP_TRY(hipSetDevice(c->device));
     if (c->d_scene) {
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -6065,6 +6109,7 @@ int rtow_scene_upload(rtow_context* c, const rtow_scene* s) {
     d.exact = L.exact ? 1u : 0u;
     d.xdepth = std::max(1u, L.xdepth);
     d.wide = (const DWide*)(b + o_wide);
+    if (!L.tsph.empty()) d.tsph = (const DSphere*)(b + o_tsph);
     d.n_wide = n_wide;
     d.wide_root = L.wide_root;
     d.wide_need = L.wide_need;

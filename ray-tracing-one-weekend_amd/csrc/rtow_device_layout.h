@@ -347,8 +347,16 @@ struct DevScene {
     uint32_t xroot;
     uint32_t exact;
     uint32_t xdepth;  // the deepest hit() recursion of the raw graph (rawDepth, <= XDEPTH): xhit's frames per thread
-    // simple scenes with a 4-wide tree (MODE 7): nodes, count, root ref and stack need
-    const DWide* wide;
+    // simple scenes with a 4-wide tree (MODE 7): nodes, count, root ref and
+    // stack need.  Grid worlds (MODE 8, never simple) use the pointer for
+    // their TOP_SPHERE runs: a = first copy in tsph, b = count (the copy's
+    // chain = the sphere's own index) -- one slot, so that no other kernel
+    // argument moves (a moved argument cost the MODE 0 kernel 0.6%: the
+    // compiler reloads arguments inside the loop rather than spill them)
+    union {
+        const DWide* wide;
+        const DSphere* tsph;
+    };
     uint32_t n_wide;
     uint32_t wide_root;
     uint32_t wide_need;

@@ -111,16 +111,18 @@ def _save(s, tmp_path):
     return p
 
 
-@pytest.mark.parametrize("grid,dtree,expect", [("1", "1", [1, 2, 2, 2, 2, 7, 3, 3, 2, 2, 5]),
+@pytest.mark.parametrize("grid,dtree,expect", [("1", "1", [1, 2, 7, 3, 3, 2, 5]),
                                                ("0", "1", [6, 3, 3, 2, 2, 5]), ("0", "0", [0, 3, 3, 2, 2, 5])])
 def test_final_scene_top_level_items(grid, dtree, expect):
     """final_ned's top-level scan (buildTop, printed by RTOW_LAYOUT_INFO).  By
     default the ground's 20 x 20 Boxes are a grid (TOP_GRID = 7, walked by
     MODE 8) and the rest of their run -- the light (a rectangle, 1) and four
-    spheres (2) -- is scanned in place; with RTOW_GRID=0 the first tree (ground
+    spheres (2, one item: a grid world scans a run of spheres in one frame as
+    one item) -- is scanned in place; with RTOW_GRID=0 the first tree (ground
     Boxes, light, spheres) runs in trace_dnodes' loop with leaf slots
     (TOP_DTREE = 6) unless RTOW_DTREE=0 sends it to the general traversal
-    (TOP_GENERIC = 0); then two media (3), two spheres (2), the cloud (5)."""
+    (TOP_GENERIC = 0); then two media (3), two spheres (2; one run item in the
+    grid world), the cloud (5)."""
     import subprocess
     import sys
     code = ("import rtow; rtow.Scene.build('final_ned', n=100, image='synthetic').check()")

@@ -126,15 +126,6 @@ def demangled_params(name):
     return dict(zip(keys, (int(v) for v in m.groups())))
 
 
-if __name__ == "__main__":
-    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
-                                                             "ray-tracing-one-weekend_amd", "librtow_hip.so")
-    for k in kernels(lib):
-        p = demangled_params(k["name"])
-        print(p or k["name"][:40], {x: k[x] for x in ("vgpr", "scratch", "vgpr_spill", "sgpr_spill", "dyn_stack",
-                                                       "lds", "calls")})
-
-
 def disasm(path, want):
     """The disassembly (text) of the kernel whose demangled template
     parameters equal `want` (a dict, e.g. {"MODE": 8, "STACK": 16, "WAVES": 4,
@@ -163,8 +154,18 @@ def disasm(path, want):
     return None
 
 
-if __name__ == "__main__":  # python tools/codeobj.py LIB MODE STACK [WAVES BS LDSN] > kernel.s
+if __name__ == "__main__":
+    # python tools/codeobj.py [LIB]                           : every kernel's resources
+    # python tools/codeobj.py LIB MODE STACK [WAVES BS LDSN] > kernel.s : one kernel's disassembly
     a = sys.argv
-    want = {"MODE": int(a[2]), "STACK": int(a[3]), "WAVES": int(a[4]) if len(a) > 4 else 4, "PROF": 0,
-            "BS": int(a[5]) if len(a) > 5 else 256, "LDSN": int(a[6]) if len(a) > 6 else 0, "DBG": 0}
-    print(disasm(a[1], want))
+    lib = a[1] if len(a) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                               "ray-tracing-one-weekend_amd", "librtow_hip.so")
+    if len(a) > 2:
+        want = {"MODE": int(a[2]), "STACK": int(a[3]), "WAVES": int(a[4]) if len(a) > 4 else 4, "PROF": 0,
+                "BS": int(a[5]) if len(a) > 5 else 256, "LDSN": int(a[6]) if len(a) > 6 else 0, "DBG": 0}
+        print(disasm(lib, want))
+    else:
+        for k in kernels(lib):
+            p = demangled_params(k["name"])
+            print(p or k["name"][:40], {x: k[x] for x in ("vgpr", "scratch", "vgpr_spill", "sgpr_spill", "dyn_stack",
+                                                           "lds", "calls")})
