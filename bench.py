@@ -88,6 +88,9 @@ def parse(argv=None):
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--texture", choices=["earth", "synthetic"], default="earth",
+                    help="earth: the reference's input_images/1_earth_8k.jpg (scenes.h:140), staged in the repo; "
+                         "synthetic: rtow_synthetic_image's 2048x1024 stand-in")
     ap.add_argument("--cpu-pixels", type=int, default=None,
                     help="pixels of the CPU baseline's sample (default: ~10-20 s of the reference's work)")
     ap.add_argument("--cpu-spp", type=int, default=None)
@@ -145,6 +148,23 @@ def launch(nproc, argv, script=None):
     return subprocess.run(cmd).returncode
 
 
+EARTH = os.path.join(REPO, "input_images", "1_earth_8k.jpg")
+
+
+def build_scene(args):
+    """The benched world: the reference's scene builder restated
+    (rtow_build_scene), with the reference's own earth texture
+    (input_images/1_earth_8k.jpg, loaded as scenes.h:140 does) unless
+    --texture synthetic."""
+    import rtow
+
+    if args.texture == "earth":
+        if not os.path.exists(EARTH):
+            raise SystemExit(f"bench: {EARTH} is missing (--texture synthetic renders without it)")
+        return rtow.Scene.build(args.scene, n=max(args.n, 1), image="jpeg", image_path=EARTH, scene_seed=1)
+    return rtow.Scene.build(args.scene, n=max(args.n, 1), image="synthetic", scene_seed=1)
+
+
 # ---------------------------------------------------------------------------
 # CPU baseline
 def reference_run(pix, args, threads, racy=False):
@@ -154,8 +174,9 @@ def reference_run(pix, args, threads, racy=False):
     harness was not built.  racy: with the reference's own shared
     std::mt19937_64 (rngs.h:9-11) instead of the seeded counter engine.  The
     scenes load their earth texture from ./input_images/1_earth_8k.jpg
-    (scenes.h:140): the synthetic texture the GPU uses is staged there as a
-    lossless PNG."""
+    (scenes.h:140): the repo's copy of that file, or with --texture synthetic
+    the synthetic texture staged there as a lossless PNG."""
+    import shutil
     import tempfile
 
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
@@ -169,8 +190,11 @@ def reference_run(pix, args, threads, racy=False):
         return None
     with tempfile.TemporaryDirectory() as d:
         os.makedirs(os.path.join(d, "input_images"))
-        Image.fromarray(rtow.synthetic_image(2048, 1024), "RGB").save(
-            os.path.join(d, "input_images", "1_earth_8k.jpg"), format="PNG")
+        if args.texture == "earth":
+            shutil.copy(EARTH, os.path.join(d, "input_images", "1_earth_8k.jpg"))
+        else:
+            Image.fromarray(rtow.synthetic_image(2048, 1024), "RGB").save(
+                os.path.join(d, "input_images", "1_earth_8k.jpg"), format="PNG")
         pf = os.path.join(d, "pix.u32")
         pix.tofile(pf)
         env = dict(os.environ, RTOW_SCENE_SEED="1")
@@ -353,7 +377,7 @@ class HipRank:
         torch.cuda.set_device(local)
         self.device = torch.device("cuda", local)
         W, H = args.width, args.height
-        self.scene = rtow.Scene.build(args.scene, n=max(args.n, 1), image="synthetic", scene_seed=1)
+        self.scene = build_scene(args)
         self.cam = rtow.camera_main(W, H)
         self.ctx = rtow.Context(local)
         self.ctx.upload(self.scene)
@@ -438,7 +462,7 @@ class InprocRank(HipRank):
         torch.cuda.set_device(0)
         self.device = torch.device("cuda", 0)
         W, H = args.width, args.height
-        self.scene = rtow.Scene.build(args.scene, n=max(args.n, 1), image="synthetic", scene_seed=1)
+        self.scene = build_scene(args)
         self.cam = rtow.camera_main(W, H)
         self.multi = rtow.Multi(list(range(self.n_gpus)))
         self.multi.upload(self.scene)
@@ -551,10 +575,13 @@ def _run(args, make_rank, line_fd):
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic",
+            "data": ("the reference's scene (seeded builder) and its own earth texture input_images/1_earth_8k.jpg"
+                     if args.texture == "earth" else "synthetic"),
             "config": {"workload": (f"randomScene_NED n={args.n} ({args.n + 1} hitables under one BvhNode), "
                                     if scene == "random_ned" else f"{label} ({scene}), ")
-                                   + f"{W}x{H}x{spp}spp, depth 50, synthetic 2048x1024 earth texture",
+                                   + f"{W}x{H}x{spp}spp, depth 50, "
+                                   + ("earth texture input_images/1_earth_8k.jpg (2048x1024 JPEG)" if args.texture == "earth"
+                                      else "synthetic 2048x1024 earth texture"),
                        "scene": scene, "width": W, "height": H, "spp": spp, "n": args.n, "scene_seed": 1,
                        "render_seed": args.seed, "baseline_config": is_baseline_cfg and not args.share_device,
                        "parallelism": (f"tiles8x8 interleaved over {n_gpus} device(s) of one process "

@@ -38,7 +38,7 @@ class OracleRank:
         self.args, self.rank, self.world = args, rank, world
         self.device = torch.device("cpu")
         W, H = args.width, args.height
-        self.scene = rtow.Scene.build(args.scene, n=max(args.n, 1), image="synthetic", scene_seed=1)
+        self.scene = bench.build_scene(args)
         self.cam = sio.RtowCamera.from_buffer_copy(bytes(rtow.camera_main(W, H)))
         self.p = sio.default_params(W, H, args.spp, seed=args.seed)
         self.idx = rtow.rank_pixels(W, H, rank, world)

@@ -10,9 +10,17 @@ its 4096x4096 frame also runs on 128-sample items.  These tests render those
 exact launches and compare a random pixel sample with the C oracle (the
 reference's recursion, main.cpp:939-955 / color.h:12-59) at the same spp.
 
+The bench renders configs 2 and 5 with the reference's own earth texture
+(input_images/1_earth_8k.jpg, scenes.h:140), so these tests do too, and add to
+the random sample pixels whose paths see the earth (found by rendering the
+slab at 2 spp with the synthetic stand-in and with the JPEG and taking the
+pixels that differ).
+
 Bar: per-channel RMS <= 1e-4 (BASELINE north_star) and at most 1 pixel per
 10^5 off by more than 1e-3.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -22,6 +30,23 @@ import scene_io as sio
 pytestmark = pytest.mark.gpu
 
 RMS_TOL = 1e-4
+EARTH = os.path.join(sio.REPO, "input_images", "1_earth_8k.jpg")
+
+
+def _earth_scene(name, n):
+    return rtow.Scene.build(name, n=n, image="jpeg", image_path=EARTH, scene_seed=1)
+
+
+def _earth_positions(ctx, name, n, W, H, rank, world, k, seed):
+    """Up to k slab positions whose 2-spp values change when the synthetic
+    texture is replaced by the earth JPEG: pixels whose paths see the earth."""
+    lins = []
+    for sc in (rtow.Scene.build(name, n=n, image="synthetic", scene_seed=1), _earth_scene(name, n)):
+        lins.append(_slab_render(ctx, sc, W, H, 2, 7, rank, world)[3])
+    idx = rtow.rank_pixels(W, H, rank, world)
+    hit = np.flatnonzero((idx >= 0) & (lins[0] != lins[1]).any(axis=1))
+    assert hit.size >= k, hit.size
+    return np.random.default_rng(seed).choice(hit, size=k, replace=False)
 
 
 def _slab_render(ctx, scene, W, H, spp, seed, rank, world):
@@ -42,10 +67,12 @@ def _slab_render(ctx, scene, W, H, spp, seed, rank, world):
     return cam, p, idx, lin.cpu().numpy().reshape(-1, 3), st, rtow.plan(p, ctx)
 
 
-def _compare(scene, cam, p, idx, lin, n_pix, seed):
+def _compare(scene, cam, p, idx, lin, n_pix, seed, extra=None):
     ok = np.flatnonzero(idx >= 0)
     rng = np.random.default_rng(seed)
     pick = rng.choice(ok, size=n_pix, replace=False)
+    if extra is not None:
+        pick = np.union1d(pick, extra)
     pix = idx[pick].astype(np.uint32)
     olin, _, oc = sio.oracle_render(scene.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
                                     sio.RtowParams.from_buffer_copy(bytes(p)), pixels=pix, threads=16)
@@ -56,42 +83,46 @@ def _compare(scene, cam, p, idx, lin, n_pix, seed):
 
 
 def test_config2_bench_frame_1024spp(gpu_ctx):
-    """Config 2 exactly as benched: randomScene_NED n=487, 1920x1080x1024,
-    seed 1, one rank, automatic chunking (128-sample items, n_big 7, a
-    128-sample halving tail in 8 chunks); 3000 random pixels vs the oracle."""
+    """Config 2 exactly as benched: randomScene_NED n=487 with the earth
+    texture, 1920x1080x1024, seed 1, one rank, automatic chunking (128-sample
+    items, n_big 7, a 128-sample halving tail in 8 chunks); 3000 random
+    pixels and 500 that see the earth vs the oracle."""
     W, H, spp = 1920, 1080, 1024
-    scene = rtow.Scene.build("random_ned", n=487, image="synthetic", scene_seed=1)
+    earth = _earth_positions(gpu_ctx, "random_ned", 487, W, H, 0, 1, 500, 5)
+    scene = _earth_scene("random_ned", 487)
     cam, p, idx, lin, st, pl = _slab_render(gpu_ctx, scene, W, H, spp, 1, 0, 1)
     assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail) == (128, 7, 128, 8), pl.as_dict()
     assert st.samples == W * H * spp
-    rms, d, oc = _compare(scene, cam, p, idx, lin, 3000, 0)
+    rms, d, oc = _compare(scene, cam, p, idx, lin, 3000, 0, extra=earth)
     n_off = int((d > 1e-3).sum())
-    print(f"BENCHED config2 1920x1080x1024: plan {pl.as_dict()} rms {rms} max|d| {d.max():.3g} "
-          f"pixels>1e-3 {n_off}/3000 bit-identical {float(np.mean(d == 0)):.4f} "
+    print(f"BENCHED config2 1920x1080x1024 (earth JPEG): plan {pl.as_dict()} rms {rms} max|d| {d.max():.3g} "
+          f"pixels>1e-3 {n_off}/{d.size} bit-identical {float(np.mean(d == 0)):.4f} "
           f"rays/sample gpu {st.segments / st.samples:.4f} oracle-sample {oc.segments / oc.samples:.4f} "
           f"kernel {st.kernel_ms:.1f} ms")
     assert np.isfinite(lin).all()
     assert (rms <= RMS_TOL).all(), rms
-    assert n_off <= int(1e-5 * 3000)
+    assert n_off <= int(1e-5 * d.size)
 
 
 def test_config5_rank_share_128_sample_items(gpu_ctx):
     """Config 5's 8-GPU split: rank 0's share of final_ned 4096x4096 at 512 spp,
     which picks 128-sample items (n_big 3 + the 128-sample tail) as the 8192-spp
-    bench share does (n_big 63); 500 random pixels of the slab vs the oracle."""
+    bench share does (n_big 63), with the earth texture; 500 random pixels of
+    the slab and 200 that see the earth vs the oracle."""
     W, H, spp = 4096, 4096, 512
-    scene = rtow.Scene.build("final_ned", n=1, image="synthetic", scene_seed=1)
+    earth = _earth_positions(gpu_ctx, "final_ned", 1, W, H, 0, 8, 200, 6)
+    scene = _earth_scene("final_ned", 1)
     cam, p, idx, lin, st, pl = _slab_render(gpu_ctx, scene, W, H, spp, 1, 0, 8)
     assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail) == (128, 3, 128, 8), pl.as_dict()
     full = rtow.plan(rtow.params(W, H, 8192, rank=0, world=8), gpu_ctx)
     assert (full.samples_per_chunk, full.n_big, full.n_tail) == (128, 63, 8)
-    rms, d, oc = _compare(scene, cam, p, idx, lin, 500, 1)
+    rms, d, oc = _compare(scene, cam, p, idx, lin, 500, 1, extra=earth)
     n_off = int((d > 1e-3).sum())
-    print(f"BENCHED config5 share 0/8 4096^2x512: plan {pl.as_dict()} rms {rms} max|d| {d.max():.3g} "
-          f"pixels>1e-3 {n_off}/500 bit-identical {float(np.mean(d == 0)):.4f} kernel {st.kernel_ms:.1f} ms")
+    print(f"BENCHED config5 share 0/8 4096^2x512 (earth JPEG): plan {pl.as_dict()} rms {rms} max|d| {d.max():.3g} "
+          f"pixels>1e-3 {n_off}/{d.size} bit-identical {float(np.mean(d == 0)):.4f} kernel {st.kernel_ms:.1f} ms")
     assert np.isfinite(lin).all()
     assert (rms <= RMS_TOL).all(), rms
-    assert n_off <= int(1e-5 * 500)
+    assert n_off <= int(1e-5 * d.size)
 
 
 @pytest.mark.parametrize("scene", ["cornell", "cornell_smoke"])

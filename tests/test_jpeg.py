@@ -38,6 +38,32 @@ def test_decode_matches_reference_stb(name):
     assert np.array_equal(got, ref)
 
 
+EARTH = os.path.join(sio.REPO, "input_images", "1_earth_8k.jpg")
+EARTH_FILE_SHA = "d046a2704f61001960af4634ae48b6b123aad4863d98db11285fbf62e19eee7c"
+EARTH_TEXEL_SHA = "45ede1416c89d1bffe600cc7835a77e052db626062e0d81ccf416d7bb533dc91"
+
+
+def test_staged_earth_texture():
+    """input_images/1_earth_8k.jpg, the texture the benched scenes load
+    (scenes.h:140), is the reference's file, and our decoder gives the texels
+    stb_image v2.22 gives (hash taken through oracle/_ref/ref_harness decode;
+    input_images/README.md); when the reference tree is here, the same file."""
+    import hashlib
+
+    data = open(EARTH, "rb").read()
+    assert hashlib.sha256(data).hexdigest() == EARTH_FILE_SHA
+    got = rtow.decode_jpeg(data)
+    assert got.shape == (1024, 2048, 3)
+    assert hashlib.sha256(got.tobytes()).hexdigest() == EARTH_TEXEL_SHA
+    ref = os.path.join(REF_IMAGES, "1_earth_8k.jpg")
+    if os.path.exists(ref):
+        assert open(ref, "rb").read() == data
+    s = rtow.Scene.build("random_ned", n=487, image="jpeg", image_path=EARTH)
+    d = sio.scene_dict(s)
+    assert len(d["images"]) == 1 and (int(d["images"][0]["nx"]), int(d["images"][0]["ny"])) == (2048, 1024)
+    assert bytes(d["texels"][: got.size]) == got.tobytes()
+
+
 def test_load_from_file_and_scene_build(tmp_path):
     """RTOW_IMAGE_JPEG: the scene builder reads the texture through the same
     decoder (random scene: the earth texture of scenes.h:140)."""

@@ -8,6 +8,7 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+EARTH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "input_images", "1_earth_8k.jpg")  # the benched scenes' texture (scenes.h:140)
 RTOW_PY = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "rtow.py")
 
 
@@ -40,7 +41,7 @@ def main():
     for name, n, W, H, s in configs:
         runs = []
         for m, env in zip(mods, envs):
-            sc = m.Scene.build(name, n=n, image="synthetic")
+            sc = m.Scene.build(name, n=n, image="jpeg", image_path=EARTH)
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             ctx = m.Context(0)

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+EARTH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "input_images", "1_earth_8k.jpg")  # the benched scenes' texture (scenes.h:140)
 sys.path[:0] = [os.path.join(HERE, "..", "tests"), os.path.join(HERE, "..", "ray-tracing-one-weekend_amd")]
 import rtow  # noqa: E402
 import scene_io as sio  # noqa: E402
@@ -116,7 +117,7 @@ def main():
     lines = []
     for k in [int(v) for v in args.configs.split(",")]:
         desc, name, n, W, H, spp, world = CONFIGS[k]
-        scene = rtow.Scene.build(name, n=max(n, 1), image="synthetic", scene_seed=1)
+        scene = rtow.Scene.build(name, n=max(n, 1), image="jpeg", image_path=EARTH, scene_seed=1)  # as bench.py
         ctx.upload(scene)
         cam = rtow.camera_main(W, H)
         slab = torch.zeros(rtow.rank_tile_count(W, H, 0, world) * 64 * 4, dtype=torch.uint8, device="cuda")

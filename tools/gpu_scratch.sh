@@ -1,4 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-AB_SPP=256 AB_ROUNDS=5 AB_SPC=0 AB_SCENES=cornell,cornell_smoke timeout -k 10 500 python -u tools/ab.py ab/u_minreg/librtow_hip.so ab/k2minreg/librtow_hip.so ab/k2mmc/librtow_hip.so ab/k5minreg/librtow_hip.so ab/k5mmc/librtow_hip.so > gpurun_out/ab_sched_r05.txt 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_benched_path.py -x -v -s --timeout 300 --timeout-method thread > gpurun_out/benched_path_earth.txt 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_earth.json 2> gpurun_out/bench_earth.err || exit $?

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+EARTH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "input_images", "1_earth_8k.jpg")  # the benched scenes' texture (scenes.h:140)
 sys.path.insert(0, os.path.join(REPO, "ray-tracing-one-weekend_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 import rtow  # noqa: E402
@@ -35,7 +36,7 @@ worlds = [int(v) for v in os.environ.get("RS_WORLDS", "1,2,4,8").split(",")]
 check = int(os.environ.get("RS_CHECK", "0"))
 threads = int(os.environ.get("RS_THREADS", "16"))
 torch.cuda.init()
-scene = rtow.Scene.build(SCENE, n=487 if SCENE == "random_ned" else 1, image="synthetic", scene_seed=1)
+scene = rtow.Scene.build(SCENE, n=487 if SCENE == "random_ned" else 1, image="jpeg", image_path=EARTH, scene_seed=1)
 cam = rtow.camera_main(W, H)
 ctx = rtow.Context(0)
 ctx.upload(scene)
