@@ -249,7 +249,8 @@ def test_bench_multiprocess_ranks_sharing_the_gpu(tmp_path, gpu_ctx):
     line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
     print("share-device bench:", {k: line[k] for k in ("value", "n_gpus", "ranks", "rays_per_step", "rank_kernel_ms")})
     assert line["ranks"] == 2 and line["n_gpus"] == 1 and len(line["rank_kernel_ms"]["per_rank"]) == 2
-    sc = rtow.Scene.build("random_ned", n=487, image="synthetic", scene_seed=1)
+    sc = rtow.Scene.build("random_ned", n=487, image="jpeg", scene_seed=1,  # the bench's earth texture
+                          image_path=os.path.join(repo, "input_images", "1_earth_8k.jpg"))
     gpu_ctx.upload(sc)
     bgra, _, st = gpu_ctx.render(rtow.camera_main(W, H), rtow.params(W, H, spp, seed=1), linear=False)
     assert line["rays_per_step"] == st.segments

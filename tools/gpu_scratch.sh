@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_benched_path.py -x -v -s --timeout 300 --timeout-method thread > gpurun_out/benched_path_earth.txt 2>&1 || exit $?
-timeout -k 10 300 python -u bench.py > gpurun_out/bench_earth.json 2> gpurun_out/bench_earth.err || exit $?
+bash tools/round_check.sh r05 configs,validate || exit $?
+RS_SCENE=final_ned RS_WORLDS=8 RS_CHECK=1000 timeout -k 10 400 python -u tools/rank_share.py > gpurun_out/rank_share_final_ned_r05.txt 2>&1 || exit $?

@@ -15,6 +15,7 @@ import time
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+EARTH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "input_images", "1_earth_8k.jpg")  # the benched scenes' texture (scenes.h:140)
 sys.path[:0] = [os.path.join(HERE, "..", "tests"), os.path.join(HERE, "..", "ray-tracing-one-weekend_amd")]
 import rtow  # noqa: E402
 import scene_io as sio  # noqa: E402
@@ -36,7 +37,7 @@ def main():
     lines = []
     cases = [c for c in CASES if args.scenes is None or c[0] in args.scenes.split(",")]
     for name, n, W, H, spp in cases:
-        scene = rtow.Scene.build(name, n=max(n, 1), image="synthetic", scene_seed=1)
+        scene = rtow.Scene.build(name, n=max(n, 1), image="jpeg", image_path=EARTH, scene_seed=1)  # as bench.py
         ctx.upload(scene)
         cam = rtow.camera_main(W, H)
         p = rtow.params(W, H, spp, seed=7)
