@@ -256,6 +256,8 @@ typedef struct rtow_build_opts {
     const char* image_path;
     uint32_t image_nx, image_ny;
     uint32_t wrap_world;       /* 1: add main.cpp's root Translate (main.cpp:132/136) */
+    uint32_t ground_side;      /* final_ned: the ground's Boxes per side over the same 2000 x 2000
+                                  (0: the book's 20; tests use larger grids) */
 } rtow_build_opts;
 
 typedef struct rtow_scene_buf rtow_scene_buf; /* owns the arrays an rtow_scene views */
@@ -436,7 +438,14 @@ int rtow_assemble_linear_device(rtow_context* ctx, uint32_t width, uint32_t heig
  * The frame equals rtow_render's bit for bit for any n: the RNG is keyed by
  * global pixel and sample, and the pixel sums are exact.  HIP failures return
  * RTOW_E_HIP, RCCL failures RTOW_E_RCCL (ncclResult text in rtow_last_error).
- * `devices`: n distinct HIP device indices, device 0 of the list gathers. */
+ * `devices`: n HIP device indices; the first entry's device gathers.
+ * A device may be listed more than once: it then holds that many ranks (each
+ * its own context and stream on the device, rendering at once), and because
+ * RCCL allows one rank per device the WHOLE gather then uses device copies
+ * (hipMemcpyPeerAsync into the first entry's slots) instead of RCCL, for
+ * every entry, distinct ones included.  The frame is the same; the render is
+ * an oversubscribed one (meant for running the n-rank path on fewer GPUs),
+ * so list each device once for a real multi-GPU render. */
 typedef struct rtow_multi rtow_multi;
 int rtow_multi_create(const int* devices, uint32_t n_devices, rtow_multi** out);
 int rtow_multi_destroy(rtow_multi* m);

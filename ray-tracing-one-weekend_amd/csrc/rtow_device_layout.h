@@ -75,20 +75,6 @@ struct alignas(16) DNode {
     uint32_t ref_b;
 };
 
-// The 4-wide tree of a simple scene (MODE 7, RTOW_WIDE): every node is either
-// INNER -- up to four child boxes, x/y/z planes as SoA (lo_x[4] hi_x[4]
-// lo_y[4] hi_y[4] lo_z[4] hi_z[4] in f[0..23]), children referenced by ref[k]
-// (DK_BVH: an inner node, DK_LIST: a leaf node, DK_NONE: empty, its box empty)
-// -- or LEAF -- up to four spheres, k-th at f[4k..4k+3] = center0 xyz, r*r and
-// f[16+3k..18+3k] = center1 - center0, ref[k] = DK_SPHERE | sphere index
-// (DK_NONE after the last).  A step of the traversal runs one kind of work
-// for every lane at that kind of node: four slab tests, or a loop of sphere
-// tests.
-struct alignas(16) DWide {  // 128 B
-    float f[28];
-    uint32_t ref[4];
-};
-
 // Sphere (sphere.h:7-18) and MovingSphere (sphere.h:76-91) share one leaf:
 // a static sphere is stored with center1 = center0, time0 = 0, time1 = 1, and
 // center(time) = c0 + ((time-0)/(1-0)) * (c0-c0) = c0 exactly, so one test
@@ -283,6 +269,14 @@ struct alignas(16) DImage {
     uint64_t offset;
 };
 
+// DevScene::root_chain: the instances above a simple scene's BvhNode tree
+constexpr int ROOTCHAIN = 4;
+// MODE 8 at STACK 16 stages the grids' packed cell heights (DevScene::gq) in
+// LDS after the COLD words when they fit in this many words (4 blocks of 256
+// threads then take 4 x 40 KB of the CU's 160 KB); larger tables go to the
+// STACK 20 kernel, which reads them from global memory.
+constexpr uint32_t GRID_LDS_WORDS = 512;
+
 // Pointers into one device allocation + scene-wide facts the launch needs.
 struct DevScene {
     const DBvh* bvh;
@@ -335,7 +329,7 @@ struct DevScene {
     uint32_t simple;
     uint32_t unit_time;      // every sphere has time0 = 0, time1 = 1
     uint32_t root_chain_n;
-    uint32_t root_chain[4];
+    uint32_t root_chain[ROOTCHAIN];
     uint32_t bvh_root;       // root below the chain
     uint32_t n_node;         // DNode count (simple scenes)
     float tshift[3];         // simple scenes: world-frame offset of the DNode boxes (shiftBoxes)
@@ -347,19 +341,14 @@ struct DevScene {
     uint32_t xroot;
     uint32_t exact;
     uint32_t xdepth;  // the deepest hit() recursion of the raw graph (rawDepth, <= XDEPTH): xhit's frames per thread
-    // simple scenes with a 4-wide tree (MODE 7): nodes, count, root ref and
-    // stack need.  Grid worlds (MODE 8, never simple) use the pointer for
-    // their TOP_SPHERE runs: a = first copy in tsph, b = count (the copy's
-    // chain = the sphere's own index) -- one slot, so that no other kernel
-    // argument moves (a moved argument cost the MODE 0 kernel 0.6%: the
-    // compiler reloads arguments inside the loop rather than spill them)
-    union {
-        const DWide* wide;
-        const DSphere* tsph;
-    };
-    uint32_t n_wide;
-    uint32_t wide_root;
-    uint32_t wide_need;
+    // grid worlds (MODE 8): copies of the top-level spheres, by run -- a
+    // TOP_SPHERE run item has a = first copy, b = count (the copy's chain = the
+    // sphere's own index)
+    const DSphere* tsph;
+    // (unused: keep every kernel argument where the measured builds had it --
+    // a moved argument cost the MODE 0 kernel 0.6 %, the compiler reloads
+    // arguments inside the loop rather than spill them)
+    uint32_t spare[3];
 };
 
 // One reference Hitable, as rtow_hitable (include/rtow.h) lays it out.

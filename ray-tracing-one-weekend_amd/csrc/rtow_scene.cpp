@@ -521,17 +521,19 @@ Hitable* threeSphere_NED(World& w) {
 // its vertical axis.  Draws in this order: 400 box heights, then per cloud
 // sphere book x, y, z; plus one per BvhNode (oracle/ref_harness.cpp
 // finalSceneNed is the same composition over the reference's own classes).
-Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth) {
+// per_side: the ground's Boxes per side (the book: 20, each 100 wide; other
+// counts keep the ground's 2000 x 2000 extent -- a larger grid for tests).
+Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth, int per_side = 20) {
     Arena& A = w.arena;
     std::vector<Hitable*> L;
-    Hitable** boxes = A.list(400);
+    Hitable** boxes = A.list((size_t)per_side * per_side);
     Hitable** cloud = A.list(1000);
     Material* white = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.73f, 0.73f, 0.73f)));
     Material* ground = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.48f, 0.83f, 0.53f)));
     int b = 0;
-    for (int i = 0; i < 20; i++) {
-        for (int j = 0; j < 20; j++) {
-            float wd = 100;
+    for (int i = 0; i < per_side; i++) {
+        for (int j = 0; j < per_side; j++) {
+            float wd = 2000.0f / (float)per_side;  // (exactly 100 for the book's 20)
             float x0 = -1000 + i * wd;
             float z0 = -1000 + j * wd;
             float x1 = x0 + wd;
@@ -634,7 +636,8 @@ int buildWorld(int sceneId, const rtow_build_opts& o, World& out) {
         if (o.wrap_world) scene = A.make<Translate>(scene, vec3(800, 0, 0));
         break;
     case RTOW_SCENE_FINAL_NED:
-        scene = finalScene_NED(out, rng, earth);
+        if (o.ground_side > 256) return set_error(RTOW_E_INVALID, "final scene: at most 256 ground Boxes per side");
+        scene = finalScene_NED(out, rng, earth, o.ground_side ? (int)o.ground_side : 20);
         if (o.wrap_world) scene = A.make<Translate>(scene, vec3(600, -278, 278));
         break;
     default:

@@ -71,7 +71,7 @@ class Plan(ctypes.Structure):
 class BuildOpts(ctypes.Structure):
     _fields_ = [("scene_seed", ctypes.c_uint64), ("n", ctypes.c_uint32), ("image_mode", ctypes.c_uint32),
                 ("image_path", ctypes.c_char_p), ("image_nx", ctypes.c_uint32), ("image_ny", ctypes.c_uint32),
-                ("wrap_world", ctypes.c_uint32)]
+                ("wrap_world", ctypes.c_uint32), ("ground_side", ctypes.c_uint32)]
 
 
 class RtowError(RuntimeError):
@@ -312,7 +312,7 @@ class Scene:
 
     @classmethod
     def build(cls, scene="random_ned", n=100, image="synthetic", scene_seed=1, wrap_world=True, image_path=None,
-              image_size=(0, 0)):
+              image_size=(0, 0), ground_side=0):
         o = BuildOpts()
         lib().rtow_build_opts_default(ctypes.byref(o))
         o.scene_seed = scene_seed
@@ -321,6 +321,7 @@ class Scene:
         o.image_path = image_path.encode() if image_path else None
         o.image_nx, o.image_ny = image_size
         o.wrap_world = 1 if wrap_world else 0
+        o.ground_side = ground_side
         h = ctypes.c_void_p()
         check(lib().rtow_build_scene(SCENES[scene], ctypes.byref(o), ctypes.byref(h)), "rtow_build_scene")
         return cls(h.value)

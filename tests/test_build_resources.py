@@ -31,7 +31,7 @@ LIB = os.path.join(HERE, "..", "ray-tracing-one-weekend_amd", "librtow_hip.so")
 # variants: 12 / 8 B since trace_dnodes tests leaf slots in place, TOP_DTREE --
 # cornell unchanged, A/B; the config-5 kernel, MODE 5 at STACK 16, has none:
 # test_config5_kernel_has_no_scratch)
-SCRATCH_BOUND = {0: 0, 2: 12, 4: 24, 3: 96, 5: 12, 6: 0, 7: 24, 8: 32}  # 7: the 4-wide tree (RTOW_WIDE, experiment)
+SCRATCH_BOUND = {0: 0, 2: 12, 4: 24, 3: 96, 5: 12, 6: 0, 8: 32}
 # (5: 12 B at STACK 20 / 32 since round 5 -- chain_ray loads an instance chain's first two entries with its
 # count, one scalar round trip, A/B cornell +0.8 %; STACK 16, configs 3 and 4, keeps 0)
 # (8: MODE 5 with the grid walk, TOP_GRID: config 5's kernel since round 4, 12 B at STACK 16; 32 B at 20 and 32
@@ -86,10 +86,9 @@ def test_default_kernels_scratch_bounded(kernels):
 
 
 def built_modes(kernels):
-    """The MODEs the default build holds: 0, 2-6, 8; 7 (the 4-wide tree) only in
-    an EXPERIMENTS=1 build (measured slower, not shipped by default)."""
+    """The MODEs the build holds: 0, 2-6, 8 (no experiment kernels)."""
     modes = {codeobj.demangled_params(k["name"])["MODE"] for k in kernels if codeobj.demangled_params(k["name"])}
-    assert {0, 2, 3, 4, 5, 6, 8} <= modes <= {0, 2, 3, 4, 5, 6, 7, 8}
+    assert modes == {0, 2, 3, 4, 5, 6, 8}
     return modes
 
 

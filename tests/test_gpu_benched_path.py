@@ -104,6 +104,69 @@ def test_config2_bench_frame_1024spp(gpu_ctx):
     assert n_off <= int(1e-5 * d.size)
 
 
+def test_config2_eight_gpu_shares_1024spp(gpu_ctx):
+    """The launches an 8-GPU run of config 2 times: bench.py
+    at N > 1 plans every rank's share by itself (no RTOW_FLAG_FRAME_PLAN), so
+    each of the eight ranks cuts 32-sample items (n_big 31, a 32-sample halving
+    tail in 6 chunks) and sums them in float in sample order (main.cpp:939-946).
+    All eight shares of 1920x1080x1024 (earth JPEG, seed 1) are rendered with
+    rtow_render_tiles_device, assembled with rtow_assemble_linear_device (the
+    tile interleave standing for main.cpp:936's column interleave), and 2000
+    random pixels plus 300 that see the earth are compared with the oracle at
+    1024 spp.  The shares' segments must sum to the one-rank render's.  Rank 0
+    of world 4 (64-sample items, n_big 15, tail in 7) is checked the same way
+    on 1000 pixels of its slab."""
+    import torch
+
+    W, H, spp, world = 1920, 1080, 1024, 8
+    earth_pos = _earth_positions(gpu_ctx, "random_ned", 487, W, H, 0, 1, 300, 8)
+    earth = rtow.rank_pixels(W, H, 0, 1)[earth_pos]
+    scene = _earth_scene("random_ned", 487)
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_main(W, H)
+    stride = rtow.rank_tile_count(W, H, 0, world) * 64
+    bgra = torch.zeros((world, stride * 4), dtype=torch.uint8, device="cuda")
+    lin = torch.zeros((world, stride * 3), dtype=torch.float32, device="cuda")
+    segs, ms = 0, []
+    for r in range(world):
+        p = rtow.params(W, H, spp, seed=1, rank=r, world=world)
+        pl = rtow.plan(p, gpu_ctx)
+        assert (pl.samples_per_chunk, pl.n_big, pl.tail_samples, pl.n_tail) == (32, 31, 32, 6), (r, pl.as_dict())
+        st = gpu_ctx.render_tiles_device(cam, p, bgra[r].data_ptr(), lin[r].data_ptr())
+        torch.cuda.synchronize()
+        segs += st.segments
+        ms.append(st.kernel_ms)
+    fl = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    gpu_ctx.assemble_linear_device(W, H, world, lin.data_ptr(), stride, fl.data_ptr())
+    torch.cuda.synchronize()
+    frame = fl.cpu().numpy().reshape(-1, 3)
+    # the whole frame as one rank renders it: same paths, so the same segments
+    st1 = _slab_render(gpu_ctx, scene, W, H, spp, 1, 0, 1)[4]
+    assert segs == st1.segments, (segs, st1.segments)
+    pick = np.union1d(np.random.default_rng(10).choice(W * H, size=2000, replace=False), earth)
+    p1 = rtow.params(W, H, spp, seed=1)
+    olin, _, oc = sio.oracle_render(scene.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p1)), pixels=pick.astype(np.uint32),
+                                    threads=16)
+    g = frame[pick].astype(np.float64)
+    d = np.abs(g - olin).max(axis=1)
+    rms = np.sqrt(np.mean((g - olin) ** 2, axis=0))
+    n_off = int((d > 1e-3).sum())
+    # rank 0 of world 4
+    cam4, p4, idx4, lin4, st4, pl4 = _slab_render(gpu_ctx, scene, W, H, spp, 1, 0, 4)
+    assert (pl4.samples_per_chunk, pl4.n_big, pl4.tail_samples, pl4.n_tail) == (64, 15, 64, 7), pl4.as_dict()
+    rms4, d4, _ = _compare(scene, cam4, p4, idx4, lin4, 1000, 11)
+    print(f"BENCHED config2 8 shares 1920x1080x1024 (per-rank plan 32/31/32/6): share kernel ms "
+          f"{min(ms):.1f}..{max(ms):.1f}; rms {rms} max|d| {d.max():.3g} pixels>1e-3 {n_off}/{d.size} "
+          f"bit-identical {float(np.mean(d == 0)):.4f}; segments 8 shares {segs} = 1 rank {st1.segments}; "
+          f"world-4 rank 0 (64/15/64/7): rms {rms4} max|d| {d4.max():.3g}")
+    assert np.isfinite(frame).all()
+    assert (rms <= RMS_TOL).all(), rms
+    assert n_off <= 1
+    assert (rms4 <= RMS_TOL).all(), rms4
+    assert int((d4 > 1e-3).sum()) <= 1
+
+
 def test_config5_rank_share_128_sample_items(gpu_ctx):
     """Config 5's 8-GPU split: rank 0's share of final_ned 4096x4096 at 512 spp,
     which picks 128-sample items (n_big 3 + the 128-sample tail) as the 8192-spp

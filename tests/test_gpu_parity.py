@@ -10,7 +10,6 @@ atan2f/asinf of the sphere uv, double log/pow) and the order the path
 throughput is multiplied in (iterative vs recursive color()).
 """
 import ctypes
-import os
 
 import numpy as np
 import pytest
@@ -285,39 +284,3 @@ def test_grazing_box_edges_follow_the_reference(tree):
             assert np.array_equal(g[:, :11], o[:, :11]), (x, y, s)
     finally:
         ctx.close()
-
-
-def _wide_built():
-    import sys
-
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
-    import codeobj
-
-    return any((codeobj.demangled_params(k["name"]) or {}).get("MODE") == 7 for k in codeobj.kernels(rtow.LIB_PATH))
-
-
-@pytest.mark.skipif(not _wide_built(), reason="MODE 7 (4-wide tree) is built only with make EXPERIMENTS=1")
-@pytest.mark.parametrize("wide,spec", [("4", "0"), ("3", "0"), ("4", "16")])
-def test_wide_tree_gives_the_same_frame(wide, spec):
-    """The 4-wide tree of the simple scene (MODE 7, opt-in RTOW_WIDE=k: nodes of
-    four boxes or leaf clusters of <= k spheres; RTOW_SPEC=n: postponed leaves)
-    renders the binary-tree kernel's frame bit for bit (the record key settles
-    ties by sphere index whatever the tree); it is slower."""
-    W, H, spp = 96, 54, 16
-    sc = rtow.Scene.build("random_ned", n=487, image="synthetic")
-    cam, p = rtow.camera_main(W, H), rtow.params(W, H, spp, seed=17)
-    ref = rtow.Context(0)
-    ref.upload(sc)
-    _, a, sa = ref.render(cam, p)
-    ref.close()
-    os.environ["RTOW_WIDE"], os.environ["RTOW_SPEC"] = wide, spec
-    try:
-        ctx = rtow.Context(0)
-        ctx.upload(sc)
-    finally:
-        os.environ.pop("RTOW_WIDE")
-        os.environ.pop("RTOW_SPEC")
-    _, b, sb = ctx.render(cam, p)
-    ctx.close()
-    assert sa.segments == sb.segments
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))

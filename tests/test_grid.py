@@ -108,6 +108,38 @@ def test_grid_frame_equals_tree_frame(name, spec, gpu_ctx):  # (gpu_ctx: torch's
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,spec", [CAMS[0], CAMS[2]])
+def test_large_grid_from_global_memory(name, spec, gpu_ctx):
+    """a ground of 32 x 32 Boxes (1056 packed words, above the 512
+    the STACK 16 kernel stages in LDS) is still walked as a grid -- by the
+    MODE 8 STACK 20 kernel, which reads the words from global memory -- and
+    its frame equals the tree's bit for bit and the oracle's within the bar."""
+    W, H, spp = 64, 48, 8
+    scene = rtow.Scene.build("final_ned", n=1, image="synthetic", ground_side=32)
+    cam = _cam(W, H, spec)
+    p = rtow.params(W, H, spp, seed=29)
+    frames = []
+    for grid in ("1", "0"):
+        os.environ["RTOW_GRID"] = grid
+        try:
+            ctx = rtow.Context(0)
+            ctx.upload(scene)
+        finally:
+            os.environ.pop("RTOW_GRID", None)
+        _, lin, st = ctx.render(cam, p)
+        frames.append((lin.copy(), st.segments))
+        ctx.close()
+    (a, sa), (b, sb) = frames
+    olin, _, oc = sio.oracle_render(scene.view_ptr, sio.RtowCamera.from_buffer_copy(bytes(cam)),
+                                    sio.RtowParams.from_buffer_copy(bytes(p)))
+    rms = np.sqrt(np.mean((np.asarray(a, np.float64).reshape(-1, 3) - olin.astype(np.float64)) ** 2, axis=0))
+    print(f"LARGE GRID {name}: segments grid {sa} tree {sb} oracle {oc.segments} rms {rms}")
+    assert sa == sb == oc.segments
+    assert np.array_equal(a, b)
+    assert (rms <= 1e-4).all(), rms
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,spec", CAMS[1:])
 def test_grid_matches_oracle_grazing(name, spec, gpu_ctx):
     W, H, spp = 48, 36, 8

@@ -154,12 +154,45 @@ def disasm(path, want):
     return None
 
 
+def isa_digest(path):
+    """{kernel symbol: sha256 of its disassembly with addresses stripped} over
+    every code object: two builds whose digests agree run the same machine
+    code (used to check that a host-side refactor leaves the kernels alone)."""
+    import hashlib
+
+    res = {}
+    for obj in code_objects(path):
+        with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as f:
+            f.write(obj)
+            co = f.name
+        try:
+            dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co],
+                                 capture_output=True, text=True, check=True).stdout
+        finally:
+            os.unlink(co)
+        cur, body = None, []
+        for line in dis.splitlines() + ["0 <__end__>:"]:
+            m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+            if m:
+                if cur is not None:
+                    res[cur] = hashlib.sha256("\n".join(body).encode()).hexdigest()[:16]
+                cur, body = m.group(1), []
+            elif cur is not None and line.strip():
+                # drop the address column and branch-target addresses, keep the instruction
+                body.append(re.sub(r"<[^>]*>|\b0x[0-9a-f]+\b", "", line.split("//")[0]).strip())
+    return res
+
+
 if __name__ == "__main__":
     # python tools/codeobj.py [LIB]                           : every kernel's resources
     # python tools/codeobj.py LIB MODE STACK [WAVES BS LDSN] > kernel.s : one kernel's disassembly
     a = sys.argv
     lib = a[1] if len(a) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                                "ray-tracing-one-weekend_amd", "librtow_hip.so")
+    if len(a) > 2 and a[2] == "--digest":
+        for name, h in sorted(isa_digest(lib).items()):
+            print(h, name)
+        sys.exit(0)
     if len(a) > 2:
         want = {"MODE": int(a[2]), "STACK": int(a[3]), "WAVES": int(a[4]) if len(a) > 4 else 4, "PROF": 0,
                 "BS": int(a[5]) if len(a) > 5 else 256, "LDSN": int(a[6]) if len(a) > 6 else 0, "DBG": 0}
