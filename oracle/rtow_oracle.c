@@ -50,6 +50,8 @@ typedef struct {
     rtow_oracle_counters c;
     float* trace; /* rtow_oracle_trace_sample: segment records, or NULL */
     uint32_t trace_max, trace_n;
+    float* rays;  /* rtow_oracle_trace_rays: each color() call's ray (o, d, time), or NULL */
+    uint32_t rays_max, rays_n;
 } ctx_t;
 
 static inline double unif(ctx_t* cx, rng_t* g) {
@@ -505,6 +507,13 @@ static v3 color(ctx_t* cx, rng_t* g, const rtow_params* P, const ray_t* r, int d
     memset(&rec, 0, sizeof rec);
     cx->c.segments++;
     const int hit_any = hit(cx, g, cx->s->root, r, 0.001f, FLT_MAX, &rec);
+    if (cx->rays && cx->rays_n < cx->rays_max) {
+        float* o = cx->rays + (size_t)cx->rays_n * 7;
+        o[0] = r->o.x, o[1] = r->o.y, o[2] = r->o.z;
+        o[3] = r->d.x, o[4] = r->d.y, o[5] = r->d.z;
+        o[6] = r->time;
+        cx->rays_n++;
+    }
     if (cx->trace && cx->trace_n < cx->trace_max) {
         float* o = cx->trace + (size_t)cx->trace_n * RTOW_DEBUG_SEG_FLOATS;
         o[0] = hit_any ? 1.0f : 0.0f;
@@ -719,6 +728,21 @@ int rtow_oracle_trace_sample(const rtow_scene* scene, const rtow_camera* cam, co
     cx.trace_max = max_segments;
     (void)sample_color(&cx, cam, p, (int)x, (int)(p->height - 1 - y), sample);
     if (n_segments) *n_segments = cx.trace_n;
+    return 0;
+}
+
+int rtow_oracle_trace_rays(const rtow_scene* scene, const rtow_camera* cam, const rtow_params* p, uint32_t x,
+                           uint32_t y, uint32_t sample, float* out, uint32_t max_segments, uint32_t* n_segments) {
+    int rc = validate(scene, p);
+    if (rc) return rc;
+    if (!cam || !out || x >= p->width || y >= p->height || sample >= p->spp) return RTOW_E_INVALID;
+    ctx_t cx;
+    memset(&cx, 0, sizeof cx);
+    cx.s = scene;
+    cx.rays = out;
+    cx.rays_max = max_segments;
+    (void)sample_color(&cx, cam, p, (int)x, (int)(p->height - 1 - y), sample);
+    if (n_segments) *n_segments = cx.rays_n;
     return 0;
 }
 

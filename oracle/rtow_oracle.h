@@ -65,6 +65,12 @@ int rtow_oracle_camera_ray(const rtow_camera* cam, const rtow_params* p, uint32_
  * RTOW_DEBUG_SEG_FLOATS floats, the records rtow_debug_trace_sample writes. */
 int rtow_oracle_trace_sample(const rtow_scene* scene, const rtow_camera* cam, const rtow_params* p, uint32_t x,
                              uint32_t y, uint32_t sample, float* out, uint32_t max_segments, uint32_t* n_segments);
+/* The rays of the same sample's color() calls (world frame, in call order):
+ * 7 floats each, origin xyz, direction xyz, time -- the rays the device's
+ * traversal is handed (tools/regroup_emulate.py prices traversal orders on
+ * them). */
+int rtow_oracle_trace_rays(const rtow_scene* scene, const rtow_camera* cam, const rtow_params* p, uint32_t x,
+                           uint32_t y, uint32_t sample, float* out, uint32_t max_segments, uint32_t* n_segments);
 
 #ifdef __cplusplus
 }
