@@ -63,8 +63,29 @@ static int sph_root(const float* s, float time, const float* o, const float* d, 
  * slot a is a sphere, bit 2 slot b's sphere has disc > 0, bit 3 the same for
  * a, bit 4 slot b's slab test hit, bit 5 slot a's.  steps[i]: the step count
  * (capped at maxs), prim[i] / bt[i]: the record. */
+int trace_rays_seeded(const dnode* nodes, uint32_t n_nodes, uint32_t root, const float* tshift, const float* rays,
+                      int n, uint8_t* codes, int maxs, int* steps, uint32_t* prim, float* bt_out, const float* seed_t,
+                      const uint32_t* seed_ref);
 int trace_rays(const dnode* nodes, uint32_t n_nodes, uint32_t root, const float* tshift, const float* rays, int n,
                uint8_t* codes, int maxs, int* steps, uint32_t* prim, float* bt_out) {
+    return trace_rays_seeded(nodes, n_nodes, root, tshift, rays, n, codes, maxs, steps, prim, bt_out, 0, 0);
+}
+
+/* Sphere::hit of one sphere (c0, radius^2, dc as a DNode slot holds them) for
+ * ray i: the root or -1 (the seed a lane could take from a predicted sphere) */
+float sphere_t(const float* slot, const float* R) {
+    const float o[3] = {R[0], R[1], R[2]}, d[3] = {R[3], R[4], R[5]};
+    const float a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+    float t;
+    int dp;
+    return sph_root(slot, R[6], o, d, a, 0.001f, &t, &dp) ? t : -1.0f;
+}
+
+/* The same with a seed per ray (seed_ref NONE: none): the record starts as
+ * that sphere's hit, as if the lane had tested it before the traversal. */
+int trace_rays_seeded(const dnode* nodes, uint32_t n_nodes, uint32_t root, const float* tshift, const float* rays,
+                      int n, uint8_t* codes, int maxs, int* steps, uint32_t* prim, float* bt_out, const float* seed_t,
+                      const uint32_t* seed_ref) {
     for (int i = 0; i < n; i++) {
         const float* R = rays + 7 * (size_t)i;
         const float o[3] = {R[0], R[1], R[2]}, d[3] = {R[3], R[4], R[5]};
@@ -82,6 +103,10 @@ int trace_rays(const dnode* nodes, uint32_t n_nodes, uint32_t root, const float*
         const float tmin = 0.001f;
         float bt = 3.4028235e38f;
         uint32_t best = NONE;
+        if (seed_ref && seed_ref[i] != NONE) {
+            bt = seed_t[i];
+            best = seed_ref[i];
+        }
         float btc = cull_bound(bt) + werr;
         unsigned long long rkey = (unsigned long long)f2u(bt) << 32 | (uint32_t)~best;
         uint32_t stack[128];
