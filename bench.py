@@ -330,6 +330,10 @@ def roofline(args, world, launch_rays, mean_kms, bpr, src_hash):
     if bpr is not None:
         roof["reference_bytes_per_ray"] = round(bpr, 1)
         roof["reference_equiv_gbps"] = round(bpr * launch_rays / (mean_kms * 1e-3) / 1e9, 1)
+    roof["bound_note"] = ("VALU issue bounds this kernel, not HBM: the scene is LDS/L2-resident (hbm_frac is the "
+                          "measured DRAM traffic over 8 TB/s); reference_equiv_gbps prices the record bytes the "
+                          "reference's exhaustive traversal reads (SURVEY 8d), which the SAH traversal never "
+                          "fetches -- informational, not a hardware bound (DESIGN.md 'Roofline and measurement')")
     return roof
 
 

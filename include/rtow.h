@@ -237,8 +237,12 @@ enum {
     RTOW_SCENE_RANDOM_NED = 2,    /* randomScene_NED scenes.h:122-218, n parameterised */
     RTOW_SCENE_CORNELL_NED = 3,   /* cornellBox_NED scenes.h:355-483 */
     RTOW_SCENE_CORNELL_SMOKE = 4, /* cornellBox_NED + smoke box of scenes.h:461-470 */
-    RTOW_SCENE_FINAL_NED = 5      /* config 5: book 2's final scene composed from the reference's
+    RTOW_SCENE_FINAL_NED = 5,     /* config 5: book 2's final scene composed from the reference's
                                      classes in NED; root Translate (600,-278,278) */
+    RTOW_SCENE_RANDOM = 6,        /* randomScene scenes.h:29-120 (not NED; no root Translate: main.cpp
+                                     renders the NED builders), n parameterised; its image is
+                                     input_images/earth1300x1300.jpg (scenes.h:47) */
+    RTOW_SCENE_CORNELL = 7        /* cornellBox scenes.h:220-353 (not NED; no root Translate) */
 };
 
 enum {
@@ -279,6 +283,14 @@ int rtow_camera_main(uint32_t width, uint32_t height, rtow_camera* out);
  * as setCamera_QuaternionMatrix (camera.h:315-342) forms it. */
 int rtow_camera_oriented(uint32_t width, uint32_t height, const float look_from[3], const float rows[9],
                          rtow_camera* out);
+/* Camera(lookFrom, lookAt, up, vFoV, aspect, aperture, focusDistance, t0, t1)
+ * with the basis of setCamera_Euler (camera.h:271-313: w = unit(lookFrom -
+ * lookAt), u = unit(cross(up, w)), v = cross(w, u)), the classic look-at
+ * camera; the reference's setCamera() compiles it out in favour of the
+ * quaternion form (camera.h:344-350), so main.cpp never sees it. */
+int rtow_camera_look_at(const float look_from[3], const float look_at[3], const float up[3], float vfov_deg,
+                        float aspect, float aperture, float focus_distance, float time0, float time1,
+                        rtow_camera* out);
 /* JPEG decoding as the reference's stb_image.h v2.22 does it (stbi_load with
  * req_comp 0, scenes.h:140): baseline and progressive Huffman, 8-bit, 1/3/4
  * components, any sampling, restart intervals; same bytes as stbi_load

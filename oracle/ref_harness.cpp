@@ -439,6 +439,11 @@ static Hitable* buildWorld(const std::string& name, const Opts& o) {
         bool used;
         return new Translate(randomSceneNedN(o.n, &used), vec3(0, 0, 1000));
     }
+    // the reference's non-NED builders, called directly (main.cpp selects the
+    // NED ones, so no root Translate): scenes.h:29-120 loads
+    // ./input_images/earth1300x1300.jpg relative to the working directory
+    if (name == "random") return randomScene();
+    if (name == "cornell_box") return cornellBox();
     if (name == "cornell") return new Translate(cornellBox_NED(), vec3(800, 0, 0));
     if (name == "cornell_smoke") return new Translate(cornellSmokeNed(), vec3(800, 0, 0));
     if (name == "three_sphere") return threeSphereNed();
@@ -634,6 +639,21 @@ int main(int argc, char** argv) {
         for (int k = 0; k < 12; k++) v[k] = (float)std::atof(argv[4 + k]);
         orientCamera(c, v);
         writeCamera(argv[16], c);
+        return 0;
+    }
+    if (cmd == "camera_euler" && argc >= 18) {
+        // setCamera_Euler (camera.h:271-313), which the reference's setCamera()
+        // compiles out (camera.h:344-350): lookFrom / lookAt / up, vfov,
+        // aspect, aperture, focus distance, t0, t1 -- the constructor, then
+        // the Euler basis on the same object (protected: public here)
+        float v[15];
+        for (int k = 0; k < 15; k++) v[k] = (float)std::atof(argv[2 + k]);
+        std::streambuf* old = std::cout.rdbuf(nullptr);  // the constructor prints its basis
+        Camera* c = new Camera(vec3(v[0], v[1], v[2]), vec3(v[3], v[4], v[5]), vec3(v[6], v[7], v[8]), v[9], v[10],
+                               v[11], v[12], v[13], v[14]);
+        std::cout.rdbuf(old);
+        c->setCamera_Euler();
+        writeCamera(argv[17], c);
         return 0;
     }
     if (cmd == "camera_check" && argc >= 16) {

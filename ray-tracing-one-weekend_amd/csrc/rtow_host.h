@@ -60,6 +60,10 @@ inline vec3 operator*(float t, const vec3& v) { return vec3(t * v.e[0], t * v.e[
 inline vec3 operator*(const vec3& v, float t) { return vec3(t * v.e[0], t * v.e[1], t * v.e[2]); }
 inline vec3 operator/(const vec3& v, float t) { return vec3(v.e[0] / t, v.e[1] / t, v.e[2] / t); }
 inline float dot(const vec3& a, const vec3& b) { return a.e[0] * b.e[0] + a.e[1] * b.e[1] + a.e[2] * b.e[2]; }
+inline vec3 cross(const vec3& v1, const vec3& v2) {  // vec3.h:90-96
+    return vec3((v1.e[1] * v2.e[2] - v1.e[2] * v2.e[1]), (-(v1.e[0] * v2.e[2] - v1.e[2] * v2.e[0])),
+                (v1.e[0] * v2.e[1] - v1.e[1] * v2.e[0]));
+}
 inline vec3 unit_vector(const vec3& v) {  // vec3.h:141-148
     if (v.length() == 0.0) return vec3(0, 0, 0);
     return v / v.length();
@@ -377,6 +381,10 @@ public:
     void setAperture(float a) { _aperture = a; setCamera(); }
     void setFocusDistance(float d) { _focusDistance = d; setCamera(); }
     void setTime(float t0, float t1) { _time0 = t0; _time1 = t1; setCamera(); }
+    // setCamera_Euler (camera.h:271-313): the basis from lookFrom, lookAt and
+    // up instead of the orientation rows (the reference compiles it out of
+    // setCamera, camera.h:344-350; here it is selectable)
+    void setCamera_Euler();
     rtow_camera toDevice() const;
 
 private:
@@ -414,7 +422,12 @@ Hitable* randomScene_NED(World& w, SceneRng& rng, int n, const Image* earth);
 Hitable* cornellBox_NED(World& w);                 // scenes.h:355-483
 Hitable* cornellSmoke_NED(World& w);               // + smoke box of scenes.h:461-470
 Hitable* threeSphere_NED(World& w);                // config 1 (composed)
-Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth);  // config 5 (composed)
+// config 5 (composed); per_side: the ground's Boxes per side (the book's 20)
+Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth, int per_side = 20);
+// the reference's non-NED builders: randomScene scenes.h:29-120 (n
+// parameterised, `earth` its earth1300x1300.jpg) and cornellBox scenes.h:220-353
+Hitable* randomScene(World& w, SceneRng& rng, int n, const Image* earth);
+Hitable* cornellBox(World& w);
 
 // Build one of the RTOW_SCENE_* worlds the way main.cpp does (Perlin tables
 // first, then the scene, then main.cpp's root Translate when opts.wrap_world).

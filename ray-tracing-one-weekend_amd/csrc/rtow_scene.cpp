@@ -362,6 +362,21 @@ void Camera::setCamera() {
     _vertical = 2 * half_height * _focusDistance * _v;
 }
 
+void Camera::setCamera_Euler() {  // camera.h:271-313
+    _lensRadius = _aperture / 2;
+    float theta = (float)(_vFoV * M_PI / 180);
+    float half_height = std::tan(theta / 2);
+    float half_width = _aspect * half_height;
+    _origin = _lookFromPoint;
+    _w = unit_vector(_lookFromPoint - _lookAt);
+    _u = unit_vector(cross(_upDirection, _w));
+    _v = cross(_w, _u);
+    _lowerLeftCorner = _origin - half_width * _focusDistance * _u - half_height * _focusDistance * _v -
+                       _focusDistance * _w;
+    _horizontal = 2 * half_width * _focusDistance * _u;
+    _vertical = 2 * half_height * _focusDistance * _v;
+}
+
 rtow_camera Camera::toDevice() const {
     rtow_camera c{};
     put3(c.origin, _origin);
@@ -449,6 +464,90 @@ Hitable* randomScene_NED(World& w, SceneRng& rng, int n, const Image* earth) {  
     return A.make<BvhNode>(A, rng, list, i, 0.0f, 1.0f);
 }
 
+// scenes.h:29-120, the reference's first random scene (its own frame, no
+// root Translate: main.cpp renders the NED builders), n parameterised like
+// randomScene_NED (the reference hard-codes 100).  The same draws in the same
+// (g++: right-to-left argument) order as the reference.
+Hitable* randomScene(World& w, SceneRng& rng, int n, const Image* earth) {
+    Arena& A = w.arena;
+    Hitable** list = A.list((size_t)n + 1);
+    Texture* checker = A.make<CheckerTexture>(A.make<ConstantTexture>(vec3(0.2f, 0.2f, 0.8f)),
+                                              A.make<ConstantTexture>(vec3(0.9f, 0.9f, 0.9f)));
+    Texture* perlin = A.make<NoiseTexture>(true, 8.0f);
+    Material* emitterMat = A.make<DiffuseLight>(A.make<ConstantTexture>(vec3(20 * 1, 20 * 0, 20 * 0)));
+    Material* imageMat = nullptr;  // scenes.h:47: ./input_images/earth1300x1300.jpg
+    if (earth && !earth->empty())
+        imageMat = A.make<Lambertian>(A.make<ImageTexture>(earth->rgb.data(), earth->nx, earth->ny));
+    list[0] = A.make<Sphere>(vec3(0, 1000, 0), 1000.0f, A.make<Lambertian>(perlin));
+    int i = 1;
+    const int xMod = 5, yMod = 5;
+    int cx = -xMod, cy = -yMod;
+    while (i < n - 3) {
+        float choose = (float)rng();
+        double uz = rng();  // vec3(x, y, z)'s arguments right to left: z's draw first
+        double ux = rng();
+        vec3 center((float)(cx + 0.9 * ux), -0.2f, (float)(cy + 0.9 * uz));
+        if ((center - vec3(4, 0.2f, 0)).length() > 0.9) {
+            if (choose < 0.8) {
+                double up = rng();
+                list[i++] = A.make<MovingSphere>(center, center + vec3(0, (float)(0.5 * up), 0), 0.0f, 1.0f, 0.2f,
+                                                 A.make<Lambertian>(checker));
+            } else if (choose < 0.95) {
+                double az = rng(), ay = rng(), ax = rng(), fz = rng();
+                list[i++] = A.make<Sphere>(
+                    center, 0.2f,
+                    A.make<Metal>(vec3((float)(0.5 * (1 + ax)), (float)(0.5 * (1 + ay)), (float)(0.5 * (1 + az))),
+                                  (float)(0.5 * (1 + fz))));
+            } else {
+                list[i++] = A.make<Sphere>(center, 0.2f, A.make<Dielectric>(1.5f));
+            }
+        }
+        if (cx < xMod) {
+            cx++;
+        } else {
+            cx = -xMod;
+            cy++;
+        }
+        if (cy > yMod) cy = -yMod;
+    }
+    if (imageMat)
+        list[i++] = A.make<Sphere>(vec3(0, -2.0f, 20), 2.0f, imageMat);
+    else
+        list[i++] = A.make<Sphere>(vec3(5, -1.0f, 0), 1.0f, A.make<Dielectric>(1.5f));
+    list[i++] = A.make<Sphere>(vec3(-4, -1.0f, 0), 1.0f, A.make<Lambertian>(perlin));
+    list[i++] = A.make<Sphere>(vec3(4, -1.0f, 0), 1.0f, A.make<Metal>(vec3(0.7f, 0.6f, 0.5f), 0.0f));
+    list[i++] = A.make<Sphere>(vec3(0, -400, 10), 100.0f, emitterMat);  // the "sun"
+    return A.make<BvhNode>(A, rng, list, i, 0.0f, 1.0f);
+}
+
+// scenes.h:220-353, the reference's first Cornell box (its own frame, no root
+// Translate): the light, five walls (the back one under Translate(0, 0, 0)),
+// the medium inside the glass sphere.  The reference computes the extents in
+// int arithmetic (planeWidth = planeHeight = planeAxisDepthOffset = 500,
+// xCoord = yCoord = 0); these are its values.
+Hitable* cornellBox(World& w) {
+    Arena& A = w.arena;
+    std::vector<Hitable*> L;
+    Material* white = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.73f, 0.73f, 0.73f)));
+    Material* red = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.65f, 0.05f, 0.05f)));
+    Material* blue = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.12f, 0.12f, 0.45f)));
+    Material* light = A.make<DiffuseLight>(A.make<ConstantTexture>(vec3(3, 3, 3)));
+    L.push_back(A.make<XZRectangle>(-175, 175, 75, 425, -249, light));                           // light panel
+    L.push_back(A.make<XZRectangle>(-250, 250, 0, 500, -250, white));                            // top
+    L.push_back(A.make<YZRectangle>(-250, 250, 0, 500, -250, red));                              // left
+    L.push_back(A.make<Translate>(A.make<FlipNormals>(A.make<XYRectangle>(-250, 250, -250, 250, 500, white)),
+                                  vec3(0, 0, 0)));                                               // back
+    L.push_back(A.make<FlipNormals>(A.make<YZRectangle>(-250, 250, 0, 500, 250, blue)));        // right
+    L.push_back(A.make<FlipNormals>(A.make<XZRectangle>(-250, 250, 0, 500, 250, white)));       // bottom
+    Material* innerMat = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.9f, 0.05f, 0.10f)));
+    Hitable* outer = A.make<Sphere>(vec3(-150, 150, 200), 100.0f, A.make<Dielectric>(1.5f));
+    Hitable* inner = A.make<Sphere>(vec3(-150, 150, 200), 99.0f, innerMat);
+    L.push_back(A.make<ConstantMedium>(A, inner, 0.001f, A.make<ConstantTexture>(vec3(0.8f, 0.2f, 0.1f))));
+    L.push_back(inner);
+    L.push_back(outer);
+    return A.make<HitableList>(std::move(L));
+}
+
 static void cornellItems(World& w, std::vector<Hitable*>& L) {  // scenes.h:355-480
     Arena& A = w.arena;
     Material* white = A.make<Lambertian>(A.make<ConstantTexture>(vec3(0.73f, 0.73f, 0.73f)));
@@ -523,7 +622,7 @@ Hitable* threeSphere_NED(World& w) {
 // finalSceneNed is the same composition over the reference's own classes).
 // per_side: the ground's Boxes per side (the book: 20, each 100 wide; other
 // counts keep the ground's 2000 x 2000 extent -- a larger grid for tests).
-Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth, int per_side = 20) {
+Hitable* finalScene_NED(World& w, SceneRng& rng, const Image* earth, int per_side) {
     Arena& A = w.arena;
     std::vector<Hitable*> L;
     Hitable** boxes = A.list((size_t)per_side * per_side);
@@ -587,7 +686,7 @@ int buildWorld(int sceneId, const rtow_build_opts& o, World& out) {
     Hitable* scene = nullptr;
     Arena& A = out.arena;
     const Image* earth = nullptr;
-    if (sceneId == RTOW_SCENE_RANDOM_NED || sceneId == RTOW_SCENE_FINAL_NED) {
+    if (sceneId == RTOW_SCENE_RANDOM_NED || sceneId == RTOW_SCENE_FINAL_NED || sceneId == RTOW_SCENE_RANDOM) {
         if (o.image_mode == RTOW_IMAGE_SYNTHETIC) {
             out.images.push_back(syntheticImage(2048, 1024));
             earth = &out.images.back();
@@ -627,6 +726,13 @@ int buildWorld(int sceneId, const rtow_build_opts& o, World& out) {
         if (o.wrap_world) scene = A.make<Translate>(scene, vec3(0, 0, 1000));  // main.cpp:132
         break;
     }
+    case RTOW_SCENE_RANDOM:
+        if (o.n < 4) return set_error(RTOW_E_INVALID, "random scene needs n >= 4");
+        scene = randomScene(out, rng, (int)o.n, earth);
+        break;
+    case RTOW_SCENE_CORNELL:
+        scene = cornellBox(out);
+        break;
     case RTOW_SCENE_CORNELL_NED:
         scene = cornellBox_NED(out);
         if (o.wrap_world) scene = A.make<Translate>(scene, vec3(800, 0, 0));  // main.cpp:136
@@ -824,6 +930,17 @@ int rtow_camera_oriented(uint32_t width, uint32_t height, const float look_from[
     c.setOrientationRows(vec3(rows[0], rows[1], rows[2]), vec3(rows[3], rows[4], rows[5]),
                          vec3(rows[6], rows[7], rows[8]));
     c.setLookFromPoint(vec3(look_from[0], look_from[1], look_from[2]));
+    *out = c.toDevice();
+    return RTOW_OK;
+}
+
+int rtow_camera_look_at(const float look_from[3], const float look_at[3], const float up[3], float vfov_deg,
+                        float aspect, float aperture, float focus_distance, float time0, float time1,
+                        rtow_camera* out) {
+    if (!out || !look_from || !look_at || !up) return set_error(RTOW_E_INVALID, "bad camera arguments");
+    Camera c(vec3(look_from[0], look_from[1], look_from[2]), vec3(look_at[0], look_at[1], look_at[2]),
+             vec3(up[0], up[1], up[2]), vfov_deg, aspect, aperture, focus_distance, time0, time1);
+    c.setCamera_Euler();
     *out = c.toDevice();
     return RTOW_OK;
 }

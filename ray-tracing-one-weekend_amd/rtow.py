@@ -19,9 +19,10 @@ HEADER = os.path.join(REPO, "include", "rtow.h")
 # ---- constants (include/rtow.h) ---------------------------------------------
 OK, E_INVALID, E_UNSUPPORTED, E_HIP, E_NO_DEVICE, E_IO, E_NOMEM, E_RCCL = 0, -1, -2, -3, -4, -5, -6, -7
 SCENE_THREE_SPHERE, SCENE_RANDOM_NED, SCENE_CORNELL_NED, SCENE_CORNELL_SMOKE = 1, 2, 3, 4
-SCENE_FINAL_NED = 5
+SCENE_FINAL_NED, SCENE_RANDOM, SCENE_CORNELL = 5, 6, 7
 SCENES = {"three_sphere": SCENE_THREE_SPHERE, "random_ned": SCENE_RANDOM_NED, "cornell": SCENE_CORNELL_NED,
-          "cornell_smoke": SCENE_CORNELL_SMOKE, "final_ned": SCENE_FINAL_NED}
+          "cornell_smoke": SCENE_CORNELL_SMOKE, "final_ned": SCENE_FINAL_NED,
+          "random": SCENE_RANDOM, "cornell_box": SCENE_CORNELL}  # (the last two: scenes.h's non-NED builders)
 IMAGE_NONE, IMAGE_SYNTHETIC, IMAGE_RAW, IMAGE_JPEG = 0, 1, 2, 3
 IMAGES = {"none": IMAGE_NONE, "synthetic": IMAGE_SYNTHETIC, "raw": IMAGE_RAW, "jpeg": IMAGE_JPEG}
 FLAG_STATS = 1
@@ -110,6 +111,8 @@ def lib():
         "rtow_camera_main": ([u32, u32, ctypes.POINTER(Camera)], i32),
         "rtow_camera_oriented": ([u32, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                   ctypes.POINTER(Camera)], i32),
+        "rtow_camera_look_at": ([ctypes.POINTER(ctypes.c_float)] * 3 + [ctypes.c_float] * 6 + [ctypes.POINTER(Camera)],
+                                i32),
         "rtow_render_progressive": ([vp, ctypes.POINTER(Camera), ctypes.POINTER(Params), i32, vp, vp,
                                      ctypes.POINTER(u32), ctypes.POINTER(Stats)], i32),
         "rtow_synthetic_image": ([u32, u32, vp], None),
@@ -237,6 +240,15 @@ def camera_main(width, height):
     """The camera main.cpp:111-125 builds for a width x height frame."""
     c = Camera()
     check(lib().rtow_camera_main(width, height, ctypes.byref(c)), "rtow_camera_main")
+    return c
+
+
+def camera_look_at(look_from, look_at, up, vfov_deg, aspect, aperture, focus_distance, time0=0.0, time1=1.0):
+    """Camera(...) with setCamera_Euler's look-at basis (camera.h:271-313)."""
+    f3 = lambda v: (ctypes.c_float * 3)(*v)  # noqa: E731
+    c = Camera()
+    check(lib().rtow_camera_look_at(f3(look_from), f3(look_at), f3(up), vfov_deg, aspect, aperture, focus_distance,
+                                    time0, time1, ctypes.byref(c)), "rtow_camera_look_at")
     return c
 
 

@@ -3,7 +3,10 @@
 Camera (setOrientationMatrix camera.h:231-235 + setLookFromPoint, basis by
 setCamera_QuaternionMatrix camera.h:315-342), via oracle/_ref/ref_harness
 camera_oriented.  Writes tests/golden/cam_oriented_<k>.cam and
-cameras_oriented.json (the inputs).  Usage: python3 tests/golden/make_camera_golden.py"""
+cameras_oriented.json (the inputs); and the look-at cameras of
+setCamera_Euler (camera.h:271-313, ref_harness camera_euler) as
+cam_euler_<k>.cam and cameras_euler.json.
+Usage: python3 tests/golden/make_camera_golden.py"""
 import json
 import math
 import os
@@ -31,7 +34,25 @@ CASES = [
 ]
 
 
+# look_from, look_at, up, vfov, aspect, aperture, focus distance, t0, t1
+EULER = [
+    ([13.0, 2.0, 3.0], [0.0, 0.0, 0.0], [0.0, 1.0, 0.0], 20.0, 16.0 / 9.0, 0.1, 10.0, 0.0, 1.0),  # book 1's cover
+    ([0.0, 0.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, -1.0], 60.0, 1920.0 / 1080.0, 2.0, 1000.0, 0.0, 1.0),  # main.cpp's
+    ([478.0, 278.0, -600.0], [278.0, 278.0, 0.0], [0.0, 1.0, 0.0], 40.0, 1.0, 0.0, 10.0, 0.0, 1.0),  # book 2's
+    ([0.0, 5.0, 0.0], [0.0, 0.0, 0.0], [0.0, 1.0, 0.0], 45.0, 1.5, 0.5, 5.0, 0.25, 0.75),  # up along the view: u = 0
+]
+
+
 def main():
+    eul = []
+    for k, (lf, la, up, fov, asp, ap, fd, t0, t1) in enumerate(EULER):
+        path = os.path.join(HERE, f"cam_euler_{k}.cam")
+        vals = lf + la + up + [fov, asp, ap, fd, t0, t1]
+        subprocess.run([HARNESS, "camera_euler"] + [repr(float(x)) for x in vals] + [path], check=True)
+        eul.append({"look_from": lf, "look_at": la, "up": up, "vfov": fov, "aspect": asp, "aperture": ap,
+                    "focus": fd, "t0": t0, "t1": t1, "file": os.path.basename(path)})
+    with open(os.path.join(HERE, "cameras_euler.json"), "w") as f:
+        json.dump(eul, f, indent=1)
     out = []
     for k, (W, H, lf, rows) in enumerate(CASES):
         path = os.path.join(HERE, f"cam_oriented_{k}.cam")

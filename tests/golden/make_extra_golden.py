@@ -12,7 +12,11 @@
 * medium_bvh_wrapped: media below a BvhNode behind a Translate, inside a list
   and behind RotateY(Translate(...)) (ref_harness.cpp mediumBvhWrappedNed);
 * tie_bvh_entry: a list item and a BvhNode item tied at a t where the
-  BvhNode's box is entered exactly (ref_harness.cpp tieBvhEntryNed).
+  BvhNode's box is entered exactly (ref_harness.cpp tieBvhEntryNed);
+* random_ref, random_ref_noimg, cornell_box: the reference's own non-NED
+  builders randomScene() (scenes.h:29-120; with its earth1300x1300.jpg, the
+  harness run in the reference's directory, and without it: the glass
+  fallback) and cornellBox() (scenes.h:220-353), called directly.
 
 Writes <case>.{scn,lin,bgra} (texels stripped, as make_golden.py), the
 cameras, and manifest_extra.json (`flags`: the rtow_params flags the case
@@ -45,7 +49,11 @@ CASES = [
     ("medium_nested", HARNESS, 0, "medium_nested", 100, "none", 64, 36, 64, 11),
     ("medium_bvh_wrapped", HARNESS, 0, "medium_bvh_wrapped", 100, "none", 64, 36, 64, 13),
     ("tie_bvh_entry", HARNESS, 0, "tie_bvh_entry", 100, "none", 64, 36, 16, 15),
+    ("random_ref", HARNESS, 0, "random", 100, "reference", 64, 36, 16, 17),
+    ("random_ref_noimg", HARNESS, 0, "random", 100, "none", 48, 27, 16, 19),
+    ("cornell_box", HARNESS, 0, "cornell_box", 100, "none", 48, 48, 64, 21),
 ]
+REF_DIR = "/root/reference/rayTracingOneWeekend"  # its input_images/ (read only)
 SCENE_SEED = 1
 
 
@@ -53,7 +61,7 @@ def main():
     if not (os.path.exists(HARNESS) and os.path.exists(HARNESS_DOF)):
         sys.exit("build the harnesses first: make -C oracle ref")
     tmp = tempfile.mkdtemp(prefix="rtow_dof_")
-    dirs = {"none": os.path.join(tmp, "none"), "synthetic": os.path.join(tmp, "synth")}
+    dirs = {"none": os.path.join(tmp, "none"), "synthetic": os.path.join(tmp, "synth"), "reference": REF_DIR}
     os.makedirs(dirs["none"])
     os.makedirs(os.path.join(dirs["synthetic"], "input_images"))
     write_png(os.path.join(dirs["synthetic"], "input_images", "1_earth_8k.jpg"), synthetic_image(2048, 1024))
@@ -71,7 +79,12 @@ def main():
         manifest["cases"].append(dict(name=name, harness=os.path.basename(harness), flags=flags, scene=scene, n=n, image=img, width=W, height=H, spp=spp, seed=seed,
                                       texel_bytes=ntex, texel_sha256=sha, n_hitables=hdr[2]))
         print(f"{name}: {hdr[2]} hitables")
-    with open(os.path.join(HERE, "manifest_extra.json"), "w") as f:
+    # keep the cases other generators add (make_graze_golden.py: graze_medium)
+    mpath = os.path.join(HERE, "manifest_extra.json")
+    ours = {c[0] for c in CASES}
+    if os.path.exists(mpath):
+        manifest["cases"] += [c for c in json.load(open(mpath))["cases"] if c["name"] not in ours]
+    with open(mpath, "w") as f:
         json.dump(manifest, f, indent=1)
 
 

@@ -20,7 +20,8 @@ sys.path.insert(0, os.path.join(REPO, "ray-tracing-one-weekend_amd"))
 import rtow  # noqa: E402
 
 BUILDS = [("three_sphere", 1, "none"), ("random_ned", 100, "synthetic"), ("random_ned", 487, "synthetic"),
-          ("cornell", 1, "none"), ("cornell_smoke", 1, "none"), ("final_ned", 1, "synthetic")]
+          ("cornell", 1, "none"), ("cornell_smoke", 1, "none"), ("final_ned", 1, "synthetic"),
+          ("random", 100, "none"), ("cornell_box", 1, "none")]
 
 
 def worlds():
