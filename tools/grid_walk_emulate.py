@@ -255,3 +255,113 @@ segs = saved
 tails = np.array([s[3] for s in segs if s[2]])
 print(f"steps after the last candidate: mean {tails.mean():.2f} over rays with candidates; "
       f"first-candidate steps mean {np.mean([s[2][0][0] for s in segs if s[2]]):.2f}")
+
+
+# --- the wave-wide walk: the wave enumerates its lanes' walks
+# together.  Phase R: every (lane, row) pair the lanes' row ranges hold is
+# dealt over the wave's 64 lanes (a wave prefix sum over the row counts, the
+# owner's ray read back from LDS), each testing the row band and heights and
+# yielding the row's cell range; phase C the same for every (lane, row, cell)
+# triple, a candidate flagged back to its owner; phase S each owner scans its
+# candidates in walk order, skipping those that start beyond its record.  No
+# lane waits on another's walk, but no record culls the walk either (the scans
+# come after it).  Costs per wave round: a row or cell test as the kernel's
+# step (C_STEP), plus the dealing (prefix sum over the wave, owner search,
+# owner's 16 ray words from LDS, candidate flag back): C_DEAL; per walk the
+# lanes' ray words staged to LDS: C_STAGE.
+def walk_all(o, d, tmin=0.001):
+    """Rows and cells the walk tests with no culling, and the candidates in walk order."""
+    with np.errstate(divide="ignore"):
+        inv = 1.0 / d
+    ou, ov, oh = o
+    du, dv, dh = d
+    iu, iv, ih = inv
+    u0, u1 = band(U0 - D, U0 + NU * WU + D, ou, iu)
+    v0, v1 = band(V0 - D, V0 + NV * WV + D, ov, iv)
+    h0, h1 = band(HLO - D, HHI + D, oh, ih)
+    te, tx = max(u0, v0, h0, tmin), min(u1, v1, h1)
+    if not te <= tx:
+        return 0, 0, []
+    sv, su = (-1 if dv < 0 else 1), (-1 if du < 0 else 1)
+
+    def row_of(t, back):
+        vv = t * dv + ov
+        e = 2 * D + (abs(ov) + abs(vv)) * REL
+        return int(min(max(np.floor((vv + back * e - V0) / WV), 0), NV - 1))
+
+    Eu = D + (abs(ou) + abs(tx * du)) * REL
+    Ev = D + (abs(ov) + abs(tx * dv)) * REL
+    Eh = (abs(oh) + abs(tx * dh)) * REL
+    j, jl = row_of(te, -sv), row_of(tx, sv)
+    rows = cells = 0
+    cands = []
+    for jr in range(j, jl + sv, sv):
+        rows += 1
+        vlo = jr * WV + V0
+        t0, t1 = band(vlo - Ev, vlo + WV + Ev, ov, iv)
+        ra, rb = max(t0, te), min(t1, tx)
+        if not ra <= rb:
+            continue
+        ha, hb = ra * dh + oh, rb * dh + oh
+        if max(ha, hb) + Eh < rhlo[jr] or min(ha, hb) - Eh > rhhi[jr]:
+            continue
+        ua, ub = ra * du + ou, rb * du + ou
+        ia = int(min(max(np.floor((min(ua, ub) - Eu - U0) / WU), 0), NU - 1))
+        ib = int(min(max(np.floor((max(ua, ub) + Eu - U0) / WU), 0), NU - 1))
+        for ic in (range(ia, ib + 1) if su > 0 else range(ib, ia - 1, -1)):
+            cells += 1
+            ulo = ic * WU + U0
+            c0, c1 = band(ulo - Eu, ulo + WU + Eu, ou, iu)
+            c0, c1 = max(c0, ra), min(c1, rb)
+            if not c0 <= c1:
+                continue
+            ha, hb = c0 * dh + oh, c1 * dh + oh
+            if max(ha, hb) + Eh < chlo[jr, ic] or min(ha, hb) - Eh > chhi[jr, ic]:
+                continue
+            cands.append((c0, cell_box[jr, ic]))
+    return rows, cells, cands
+
+
+C_DEAL, C_STAGE, C_SKIP = 22.0, 10.0, 6.0
+allw = []
+for pth in paths:
+    for (o, d, _, _) in pth:
+        with np.errstate(divide="ignore"):
+            inv = 1.0 / d
+        rows, cells, cands = walk_all(o, d)
+        allw.append((rows, cells, cands, inv, o))
+wr = wc = ws = wk = 0
+walks = 0
+for w0 in range(0, n - 63, 64):
+    lanes = [allw[q] for q in order[w0:w0 + 64]]
+    tr, tc = sum(L[0] for L in lanes), sum(L[1] for L in lanes)
+    if tr:
+        walks += 1
+    wr += -(-tr // 64)
+    wc += -(-tc // 64)
+    # phase S: per lane its candidates in walk order, culled by its own record
+    acts = []
+    for rows, cells, cands, inv, o in lanes:
+        bt, a = np.inf, []
+        for c0, k in cands:
+            if c0 > bt * (1 + 2 ** -9):
+                a.append(0)
+                continue
+            a.append(1)
+            t = box_t(k, o, inv, 0.001, bt)
+            if t is not None:
+                bt = t
+        acts.append(a)
+    for it in range(max(len(a) for a in acts)):
+        if any(len(a) > it and a[it] for a in acts):
+            ws += 1
+        else:
+            wk += 1
+rays = (n // 64) * 64
+cost = ((C_STEP + C_DEAL) * (wr + wc) + C_SCAN * ws + C_SKIP * wk + C_STAGE * walks) / rays
+print(f"wave-wide walk: row rounds {wr / rays * 64:.2f}, cell rounds {wc / rays * 64:.2f}, wave scans "
+      f"{ws / rays * 64:.2f} (+{wk / rays * 64:.2f} skip passes) per 64 rays; rows {sum(a[0] for a in allw) / n:.2f} and "
+      f"cells {sum(a[1] for a in allw) / n:.2f} per ray unculled, candidates {sum(len(a[2]) for a in allw) / n:.3f}; "
+      f"cost {cost:.2f} VALU wave-instr per ray (K=1 above: current walk)")
+free = (C_STEP * (wr + wc) + C_SCAN * ws + C_SKIP * wk) / rays
+print(f"  the same with the dealing and staging free: {free:.2f}; the wave scans alone: {C_SCAN * ws / rays:.2f}")
